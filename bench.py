@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FM per-row scoring (K1, hhfm_fm_score_rows) on the
+BASELINE.json configs[1] workload — "FM k=64 Frappe-shape synthetic,
+1xMI355X HIP gather+interaction kernel, fp32" — in its HBM-roofline variant
+(SURVEY.md §8d C2(ii)): 8 M users + 8 M items + the 12 Frappe context ids,
+table 16.8 M x 64 fp32 (4.3 GB, far beyond the 256 MB Infinity Cache),
+2^25 uniformly random Frappe-layout rows [user, item, daytime, isweekend,
+homework] per step and GPU, seed 1 (+rank).
+
+A step = one hhfm_fm_score_rows launch over the resident batch (inputs in
+HBM before the timed region).  Multi-GPU: one process per GPU, rows sharded
+(weak scaling, no data-path collective); value = all ranks' rows / max time.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "scored (user,ctx,item) triples/sec + HR@10, Frappe-shape, 1/2/4/8 MI355X"
+BYTES_PER_ROW_F5_K64 = 5 * 64 * 4 + 5 * 4 + 5 * 4 + 4   # 1,324 B
+HBM_PEAK_GBS = 8000.0                                   # MI355X_MICROARCH.md (spec)
+CTX_CARD = (7, 2, 3)                                    # Frappe daytime/isweekend/homework
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--rows", type=int, default=1 << 25)
+    p.add_argument("--users", type=int, default=8 << 20)
+    p.add_argument("--items", type=int, default=8 << 20)
+    p.add_argument("--k", type=int, default=64)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU-baseline time budget (0 disables)")
+    p.add_argument("--cpu-rows", type=int, default=1 << 21)
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
+    return p.parse_args()
+
+
+def make_batch(rows, n_user, n_item, k, seed, dev):
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    M = n_user + n_item + sum(CTX_CARD)
+    E = torch.empty(M, k, dtype=torch.float32, device=dev)
+    E.normal_(0.0, 0.01, generator=g)                       # tf.random_normal(0, 0.01), FM.py:153
+    w = torch.empty(M, dtype=torch.float32, device=dev).normal_(0.0, 0.01, generator=g)
+    cols = [torch.randint(0, n_user, (rows,), generator=g, device=dev, dtype=torch.int32),
+            torch.randint(n_user, n_user + n_item, (rows,), generator=g, device=dev,
+                          dtype=torch.int32)]
+    off = n_user + n_item
+    for c in CTX_CARD:
+        cols.append(torch.randint(off, off + c, (rows,), generator=g, device=dev,
+                                  dtype=torch.int32))
+        off += c
+    idx = torch.stack(cols, 1).contiguous()
+    return idx, E, w, M
+
+
+def cpu_baseline(idx, E, w, w0, out_gpu, args):
+    """Time the oracle's C restatement (OpenMP) on a bounded sample of the same
+    workload (same table, first cpu_rows rows) on this box's host cores."""
+    from oracle import cpu as ocpu
+    threads = min(len(os.sched_getaffinity(0)), 16)
+    n = min(args.cpu_rows, idx.shape[0])
+    X = idx[:n].cpu().numpy()
+    Eh = E.cpu().numpy()
+    wh = w.cpu().numpy()
+    ref = ocpu.fm_out(X, Eh, wh, w0, threads)          # warm (page-in)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        ocpu.fm_out(X, Eh, wh, w0, threads)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    m = min(n, 1 << 16)                                 # parity spot-check subset
+    got = out_gpu[:m].cpu().numpy()
+    e = Eh[X[:m].astype(np.int64)].astype(np.float64)
+    scale = (0.5 * (e.sum(1) ** 2 + (e * e).sum(1))).sum(1) + np.abs(wh[X[:m]]).sum(1) + abs(w0)
+    err = float(np.max(np.abs(got - ref[:m]) / scale))
+    cpu_name = platform.processor() or "cpu"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": reps * n / el, "unit": "triples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} rows of the same workload (same 4.3 GB table) x {reps} passes, "
+                      f"oracle/cpu_oracle.c (OpenMP) on {cpu_name}",
+            "gpu_vs_cpu_max_rel_err": err}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from hhfm_amd import ops
+
+    idx, E, w, M = make_batch(args.rows, args.users, args.items, args.k, 1 + rank, dev)
+    out = torch.empty(args.rows, dtype=torch.float32, device=dev)
+    w0 = 0.0
+    for _ in range(args.warmup):
+        ops.fm_score_rows(idx, E, w, w0, out=out)
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        ops.fm_score_rows(idx, E, w, w0, out=out)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    t = torch.tensor([el, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    el, kern_ms = float(t[0]), float(t[1])
+
+    rows_total = args.rows * world * args.steps
+    value = rows_total / el
+    bpr = 5 * args.k * 4 + 5 * 4 + 5 * 4 + 4
+    achieved = bpr * args.rows / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("rows") == args.rows and tj.get("k") == args.k:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    result = {
+        "metric": METRIC, "value": value, "unit": "triples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": "FM k=64 Frappe-shape per-row scoring (configs[1], "
+                               "HBM-roofline variant: 8M users + 8M items + 12 ctx ids)",
+                   "rows_per_gpu": args.rows, "fields": 5, "k": args.k,
+                   "table_rows": M, "table_bytes": M * args.k * 4,
+                   "parallelism": f"rows sharded x{world}, no collective"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "fm_rows_fast<5,16,f32,w>", "kernel_ms": kern_ms,
+                     "algorithmic_bytes_per_row": bpr},
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        result["cpu_baseline"] = cpu_baseline(idx, E, w, w0, out, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

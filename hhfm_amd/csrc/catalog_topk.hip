@@ -1,0 +1,507 @@
+// K2 — full-catalog scoring + fused top-K on gfx950.
+//
+//   hhfm_catalog_topk replaces FM.topk       (Newcode/FM.py:172-198)
+//                     and      OUR.topk      (Newcode/OurModel7.py:229-307)
+// Both reference graphs broadcast-multiply [B,1,k] x [1,N,k], reduce over k
+// and call tf.nn.top_k(score, 20).  Here the [B,N] score matrix never exists:
+//
+//  1. catalog_queries: one fp32 query vector per row (HHFM h = u+Σctx[+Σtime];
+//     FM q = u+f with f = Σctx and the item-independent term q·f).
+//  2. catalog_main: a workgroup = 4 waves = 128 queries x one item split.
+//     Each wave owns 32 queries; their fp32 vectors stay in VGPRs as the
+//     MFMA B operand for the whole split.  Item tiles of 32 rows stream
+//     through the A operand (one 16-B load per lane per 8 (fp32) / 16 (bf16)
+//     k, next tile prefetched while this one is multiplied) and
+//     v_mfma_f32_32x32x2_f32 — exact fp32 (each MFMA is a k-ordered fmaf
+//     chain), same 157 TF peak as the fp32 VALU — yields a 32x32 score tile.
+//     For FM one extra MFMA adds w_item + q·f.  The VALU then filters the
+//     tile against each query's current K-th score; survivors enter a
+//     per-query sorted list in LDS (single insertions when sparse, a
+//     bitonic sort + merge when dense — the first tiles of a split).
+//  3. topk_merge: per query, merge the S split lists (and, multi-GPU, the R
+//     rank lists gathered over RCCL) into the final top-K.
+// Order everywhere: score descending, item index ascending (tf.nn.top_k).
+#include "topk_common.h"
+
+namespace hhfm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kQPerWave = 32;
+constexpr int kQPerBlock = 4 * kQPerWave;
+constexpr int kTile = 32;  // items per MFMA tile
+
+// ---------------------------------------------------------------------------
+// 1. query vectors
+// ---------------------------------------------------------------------------
+template <bool BF16>
+__global__ __launch_bounds__(256) void catalog_queries(
+    const int32_t* __restrict__ qidx, int64_t B, int64_t Bpad, int ncols,
+    int mode, int ucol, int c0, int c1, int t0, int t1,
+    const char* __restrict__ E, int64_t M, int k, float* __restrict__ H,
+    float* __restrict__ cst) {
+  const int lane = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  const int esz = BF16 ? 2 : 4;
+  auto val = [&](int32_t id, int e) -> float {
+    const char* r = E + (int64_t)clamp_id(id, M) * k * esz;
+    return BF16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(r)[e])
+                : reinterpret_cast<const float*>(r)[e];
+  };
+  for (int64_t b = wave; b < Bpad; b += nwave) {
+    float part = 0.f;
+    if (b < B) {
+      const int32_t* p = qidx + b * (int64_t)ncols;
+      for (int e = lane; e < k; e += kWave) {
+        const float u = val(p[ucol], e);
+        float ctx = 0.f, tim = 0.f;
+        for (int c = c0; c < c1; ++c) ctx += val(p[c], e);
+        for (int c = t0; c < t1; ++c) tim += val(p[c], e);
+        float h;
+        if (mode == HHFM_MODE_FM) {
+          h = u + ctx;          // UserWithFeature            FM.py:177
+          part += h * ctx;      // item-independent (u+f)·f   FM.py:178-183
+        } else {
+          h = u;                // Σ[user, Σctx, Σtime]        OurModel7.py:270-292
+          if (c1 > c0) h = h + ctx;
+          if (t1 > t0) h = h + tim;
+        }
+        H[b * k + e] = h;
+      }
+    } else {
+      for (int e = lane; e < k; e += kWave) H[b * k + e] = 0.f;
+    }
+    part = group_sum<kWave>(part);
+    if (lane == 0) cst[b] = part;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2. main kernel
+// ---------------------------------------------------------------------------
+// XCD-aware bijective remap: consecutive work ids land on one XCD (blocks b
+// and b+8 share an XCD), so the workgroups sweeping one item split share L2.
+HHFM_DEV int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, slot = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+template <int KPAD>
+HHFM_DEV void insert_one(float* ls, int32_t* li, float s, int32_t it, int K) {
+  const int l = lane_id();
+  const float es = (l < KPAD) ? ls[l] : kNegInf;
+  const int32_t ei = (l < KPAD) ? li[l] : kNoIdx;
+  const int pos = __popcll(__ballot(better(es, ei, s, it)));
+  if (pos < K) {  // wave-uniform
+    const float ps = __shfl_up(es, 1, kWave);
+    const int32_t pi = __shfl_up(ei, 1, kWave);
+    const float ns = l < pos ? es : (l == pos ? s : ps);
+    const int32_t ni = l < pos ? ei : (l == pos ? it : pi);
+    if (l < KPAD) {
+      ls[l] = ns;
+      li[l] = ni;
+    }
+  }
+}
+
+template <bool BF16, int KT, int KPAD, bool FM>
+__global__ __launch_bounds__(256) void catalog_main(
+    const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
+    const char* __restrict__ E, int64_t item_row_begin, int32_t N,
+    const float* __restrict__ w, int K, int S, int tiles_per_split, int nqb,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int64_t ostride_b,
+    int64_t ostride_s, int32_t gbase) {
+  constexpr int k = BF16 ? KT * 16 : KT * 8;   // factors
+  constexpr int64_t ROWB = (int64_t)KT * 32;   // bytes per embedding row
+  constexpr int EPC = BF16 ? 8 : 4;            // k-elements per 16-B chunk
+  constexpr int kBulkMin = 128;                // candidates/tile -> bulk merge
+
+  __shared__ float lst_s[4][kQPerWave * KPAD];
+  __shared__ int32_t lst_i[4][kQPerWave * KPAD];
+  __shared__ float tb[4][kQPerWave * kTile];
+
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wid / nqb;
+  const int g = wid - split * nqb;
+  const int wv = threadIdx.x / kWave;
+  const int l = lane_id();
+  const int j = l & 31;   // query column of this lane (MFMA B/C layout)
+  const int h = l >> 5;   // k half (A/B layout) / row half (C layout)
+  const int64_t q0 = (int64_t)g * kQPerBlock + wv * kQPerWave;
+  if (q0 >= B) return;    // whole wave idle; no block-level sync below
+
+  const int ntiles = (N + kTile - 1) / kTile;
+  const int tb0 = split * tiles_per_split;
+  const int tb1 = min(tb0 + tiles_per_split, ntiles);
+  const int item_end = min(tb1 * kTile, N);
+
+  float* ls = lst_s[wv];
+  int32_t* li = lst_i[wv];
+  float* T = tb[wv];
+  for (int x = l; x < kQPerWave * KPAD; x += kWave) {
+    ls[x] = kNegInf;
+    li[x] = kNoIdx;
+  }
+
+  // B operand: this lane's query, k-slices {EPC*(2t+h) .. +EPC} for every t
+  const int64_t q = q0 + j;
+  float bq[KT][EPC];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const float4* src =
+        reinterpret_cast<const float4*>(H + q * k + (2 * t + h) * EPC);
+#pragma unroll
+    for (int v = 0; v < EPC / 4; ++v) {
+      const float4 x = src[v];
+      bq[t][4 * v + 0] = x.x; bq[t][4 * v + 1] = x.y;
+      bq[t][4 * v + 2] = x.z; bq[t][4 * v + 3] = x.w;
+    }
+  }
+  float cq = 0.f;
+  if constexpr (FM) cq = cst[q];
+  float thr = (q < B) ? kNegInf : __builtin_huge_valf();
+
+  // A operand for tile `tile`: item row (tile*32 + j), 16 B per k-chunk
+  uint4 a[KT];
+  float wi = 0.f;
+  auto load_tile = [&](int tile) {
+    int item = tile * kTile + j;
+    item = item < N ? item : N - 1;
+    const char* row = E + (item_row_begin + item) * ROWB + 16 * h;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) a[t] = *reinterpret_cast<const uint4*>(row + 32 * t);
+    if constexpr (FM) wi = w ? w[item_row_begin + item] : 0.f;
+  };
+  if (tb0 < tb1) load_tile(tb0);
+
+  for (int tile = tb0; tile < tb1; ++tile) {
+    f32x16 acc = {0};
+    const int nxt = tile + 1 < tb1 ? tile + 1 : tile;
+    float wcur = wi;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      float av[EPC];
+      if constexpr (BF16) {
+        const uint32_t r4[4] = {a[t].x, a[t].y, a[t].z, a[t].w};
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          av[2 * v] = __uint_as_float(r4[v] << 16);
+          av[2 * v + 1] = __uint_as_float(r4[v] & 0xffff0000u);
+        }
+      } else {
+        av[0] = __uint_as_float(a[t].x); av[1] = __uint_as_float(a[t].y);
+        av[2] = __uint_as_float(a[t].z); av[3] = __uint_as_float(a[t].w);
+      }
+      // rolling prefetch: chunk t of the next tile replaces the consumed one
+      {
+        int item = nxt * kTile + j;
+        item = item < N ? item : N - 1;
+        a[t] = *reinterpret_cast<const uint4*>(E + (item_row_begin + item) * ROWB +
+                                               16 * h + 32 * t);
+      }
+#pragma unroll
+      for (int e = 0; e < EPC; ++e)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
+    }
+    if constexpr (FM) {
+      // D[i][j] += w_i * 1 + 1 * (q_j·f_j)   (bias row/col folded into one MFMA)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f,
+                                                 h == 0 ? 1.f : cq, acc, 0, 0, 0);
+      int item = nxt * kTile + j;
+      item = item < N ? item : N - 1;
+      wi = w ? w[item_row_begin + item] : 0.f;
+    }
+
+    // ---- filter against the per-query K-th score ----
+    const int ibase = tile * kTile;
+    bool pass[16];
+    int count = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      pass[r] = acc[r] >= thr && ibase + row < item_end;
+      count += __popcll(__ballot(pass[r]));
+    }
+    if (count == 0) continue;
+
+    if (count <= kBulkMin) {
+      // sparse: one wave-wide sorted insertion per surviving score
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        uint64_t m = __ballot(pass[r]);
+        while (m) {
+          const int L = __builtin_ctzll(m);
+          m &= m - 1;
+          const float s = __int_as_float(
+              __builtin_amdgcn_readlane(__float_as_int(acc[r]), L));
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * (L >> 5);
+          const int qq = L & 31;
+          insert_one<KPAD>(ls + qq * KPAD, li + qq * KPAD, s, ibase + row, K);
+        }
+      }
+    } else {
+      // dense: transpose the masked tile to LDS (XOR-swizzled, conflict
+      // free), bitonic-sort each query's 32 scores, merge into its list
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        T[j * kTile + (row ^ j)] = pass[r] ? acc[r] : kNegInf;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): tile visible to the wave
+      __builtin_amdgcn_wave_barrier();
+      for (int p = 0; p < kQPerWave / 2; ++p) {
+        const int qh = 2 * p + h;
+        float s = T[qh * kTile + (j ^ qh)];
+        int32_t it = s == kNegInf ? kNoIdx : ibase + j;
+        bitonic_sort_desc<32>(s, it);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int qq = 2 * p + hh;
+          float bs = shfl_f(s, 32 * hh + j);
+          int32_t bi = shfl_i(it, 32 * hh + j);
+          if (l >= 32) { bs = kNegInf; bi = kNoIdx; }
+          float as = l < KPAD ? ls[qq * KPAD + l] : kNegInf;
+          int32_t ai = l < KPAD ? li[qq * KPAD + l] : kNoIdx;
+          merge_lists<KPAD>(as, ai, bs, bi);
+          if (l < KPAD) {
+            ls[qq * KPAD + l] = as;
+            li[qq * KPAD + l] = ai;
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (q < B) thr = ls[j * KPAD + (K - 1)];
+  }
+
+  // ---- emit this split's sorted list per query ----
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  for (int qq = 0; qq < kQPerWave; ++qq) {
+    const int64_t b = q0 + qq;
+    if (b >= B) break;
+    if (l < K) {
+      const int32_t ii = li[qq * KPAD + l];
+      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * KPAD + l];
+      out_i[b * ostride_b + split * ostride_s + l] = ii == kNoIdx ? kNoIdx : ii + gbase;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 3. merge of R sorted lists per query
+// ---------------------------------------------------------------------------
+template <int KPAD>
+__global__ __launch_bounds__(256) void topk_merge_kernel(
+    const float* __restrict__ in_s, const int32_t* __restrict__ in_i, int R,
+    int64_t B, int K, int64_t stride_r, int64_t stride_b,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i) {
+  const int l = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t b = wave; b < B; b += nwave) {
+    float as = kNegInf;
+    int32_t ai = kNoIdx;
+    for (int r = 0; r < R; ++r) {
+      const int64_t off = r * stride_r + b * stride_b;
+      float bs = l < K ? in_s[off + l] : kNegInf;
+      int32_t bi = l < K ? in_i[off + l] : kNoIdx;
+      merge_lists<KPAD>(as, ai, bs, bi);
+    }
+    if (l < K) {
+      out_s[b * K + l] = as;
+      out_i[b * K + l] = ai;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct Plan {
+  int64_t Bpad;
+  int nqb, S, tiles_per_split;
+  size_t off_H, off_cst, off_ps, off_pi, total;
+};
+
+static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
+  Plan p{};
+  p.nqb = (int)((B + kQPerBlock - 1) / kQPerBlock);
+  p.Bpad = (int64_t)p.nqb * kQPerBlock;
+  const int ntiles = (N + kTile - 1) / kTile;
+  // enough workgroups to fill 256 CUs twice, but >= 16 tiles per split so
+  // the per-split warm-up of the top-K lists stays amortised
+  const int target = 1024;
+  int S = (target + p.nqb - 1) / p.nqb;
+  const int smax = ntiles / 16 > 1 ? ntiles / 16 : 1;
+  if (S > smax) S = smax;
+  if (S < 1) S = 1;
+  p.tiles_per_split = (ntiles + S - 1) / S;
+  p.S = (ntiles + p.tiles_per_split - 1) / p.tiles_per_split;
+  size_t off = 0;
+  p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
+  p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
+  p.off_ps = off;
+  if (p.S > 1) {
+    off += align256((size_t)B * p.S * K * sizeof(float));
+    p.off_pi = off;
+    off += align256((size_t)B * p.S * K * sizeof(int32_t));
+  } else {
+    p.off_pi = off;
+  }
+  p.total = off;
+  return p;
+}
+
+template <bool BF16, int KT, int KPAD, bool FM>
+static void launch_main(const Plan& p, const float* H, const float* cst, int64_t B,
+                        const char* E, int64_t item_row_begin, int32_t N,
+                        const float* w, int K, float* os, int32_t* oi,
+                        int64_t sb, int64_t ss, int32_t gbase, hipStream_t st) {
+  hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM>), dim3(p.nqb * p.S),
+                     dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
+                     p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase);
+}
+
+template <bool BF16, int KPAD, bool FM>
+static bool dispatch_kt(int KT, const Plan& p, const float* H, const float* cst,
+                        int64_t B, const char* E, int64_t irb, int32_t N,
+                        const float* w, int K, float* os, int32_t* oi, int64_t sb,
+                        int64_t ss, int32_t gbase, hipStream_t st) {
+  switch (KT) {
+    case 1: launch_main<BF16, 1, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    case 2: launch_main<BF16, 2, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    default: return false;
+  }
+  return true;
+}
+
+static void launch_merge(const float* in_s, const int32_t* in_i, int R, int64_t B,
+                         int K, int64_t stride_r, int64_t stride_b, float* os,
+                         int32_t* oi, hipStream_t st) {
+  int64_t blocks = (B + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  if (K <= 32)
+    hipLaunchKernelGGL(topk_merge_kernel<32>, dim3((int)blocks), dim3(256), 0, st,
+                       in_s, in_i, R, B, K, stride_r, stride_b, os, oi);
+  else
+    hipLaunchKernelGGL(topk_merge_kernel<64>, dim3((int)blocks), dim3(256), 0, st,
+                       in_s, in_i, R, B, K, stride_r, stride_b, os, oi);
+}
+
+}  // namespace hhfm
+
+using namespace hhfm;
+
+extern "C" int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count,
+                                           int32_t k, int32_t K,
+                                           size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || item_count < 1 || k < 1 || K < 1 || K > 64)
+    return HHFM_EINVAL;
+  *ws_bytes = make_plan(B, item_count, k, K).total;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_catalog_topk(
+    const int32_t* qidx, int64_t B, int32_t ncols, int32_t mode,
+    int32_t user_col, int32_t ctx_begin, int32_t ctx_end, int32_t time_begin,
+    int32_t time_end, const void* E, int64_t features_M, int32_t k,
+    int32_t dtype, const float* w, int32_t item_row_begin, int32_t item_count,
+    int32_t global_item_base, int32_t K, float* top_score, int32_t* top_idx,
+    void* workspace, size_t ws_bytes, void* stream) {
+  if (B < 0 || ncols < 1 || ncols > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
+  if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
+  if (mode != HHFM_MODE_FM && mode != HHFM_MODE_HHFM) return HHFM_EINVAL;
+  if (user_col < 0 || user_col >= ncols) return HHFM_EINVAL;
+  if (ctx_begin > ctx_end || time_begin > time_end) return HHFM_EINVAL;
+  if (ctx_end > ctx_begin && (ctx_begin < 0 || ctx_end > ncols)) return HHFM_EINVAL;
+  if (time_end > time_begin && (time_begin < 0 || time_end > ncols)) return HHFM_EINVAL;
+  if (item_count < 1 || item_row_begin < 0 ||
+      (int64_t)item_row_begin + item_count > features_M)
+    return HHFM_EINVAL;
+  if (K < 1 || K > item_count) return HHFM_EINVAL;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  const bool bf16 = dtype == HHFM_BF16;
+  const int epc2 = bf16 ? 16 : 8;  // k per 16-B chunk pair (two lane halves)
+  if (k % epc2) return HHFM_EUNSUPPORTED;
+  const int KT = k / epc2;
+  if (KT > 16 || (KT & (KT - 1))) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!qidx || !E || !top_score || !top_idx) return HHFM_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(E) & 15) != 0) return HHFM_EUNSUPPORTED;
+
+  const Plan p = make_plan(B, item_count, k, K);
+  if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
+  char* ws = reinterpret_cast<char*>(workspace);
+  float* H = reinterpret_cast<float*>(ws + p.off_H);
+  float* cst = reinterpret_cast<float*>(ws + p.off_cst);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const char* Eb = reinterpret_cast<const char*>(E);
+
+  {
+    int64_t blocks = (p.Bpad + 3) / 4;
+    if (blocks > 4096) blocks = 4096;
+    if (bf16)
+      hipLaunchKernelGGL(catalog_queries<true>, dim3((int)blocks), dim3(256), 0, st,
+                         qidx, B, p.Bpad, ncols, mode, user_col, ctx_begin,
+                         ctx_end, time_begin, time_end, Eb, features_M, k, H, cst);
+    else
+      hipLaunchKernelGGL(catalog_queries<false>, dim3((int)blocks), dim3(256), 0, st,
+                         qidx, B, p.Bpad, ncols, mode, user_col, ctx_begin,
+                         ctx_end, time_begin, time_end, Eb, features_M, k, H, cst);
+  }
+
+  float* os;
+  int32_t* oi;
+  int64_t sb, ss;
+  if (p.S > 1) {
+    os = reinterpret_cast<float*>(ws + p.off_ps);
+    oi = reinterpret_cast<int32_t*>(ws + p.off_pi);
+    sb = (int64_t)p.S * K;
+    ss = K;
+  } else {
+    os = top_score;
+    oi = top_idx;
+    sb = K;
+    ss = 0;
+  }
+  const int32_t gbase = global_item_base;  // order-preserving shift
+  const bool fm = mode == HHFM_MODE_FM;
+  bool ok;
+#define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, st
+  if (K <= 32) {
+    if (bf16) ok = fm ? dispatch_kt<true, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<true, 32, false>(HHFM_MAIN_ARGS);
+    else ok = fm ? dispatch_kt<false, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<false, 32, false>(HHFM_MAIN_ARGS);
+  } else {
+    if (bf16) ok = fm ? dispatch_kt<true, 64, true>(HHFM_MAIN_ARGS) : dispatch_kt<true, 64, false>(HHFM_MAIN_ARGS);
+    else ok = fm ? dispatch_kt<false, 64, true>(HHFM_MAIN_ARGS) : dispatch_kt<false, 64, false>(HHFM_MAIN_ARGS);
+  }
+#undef HHFM_MAIN_ARGS
+  if (!ok) return HHFM_EUNSUPPORTED;
+  if (p.S > 1) {
+    launch_merge(os, oi, p.S, B, K, /*stride_r=*/K, /*stride_b=*/(int64_t)p.S * K,
+                 top_score, top_idx, st);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_topk_merge(const float* in_score, const int32_t* in_idx,
+                               int32_t R, int64_t B, int32_t K, float* out_score,
+                               int32_t* out_idx, void* stream) {
+  if (R < 1 || B < 0 || K < 1) return HHFM_EINVAL;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!in_score || !in_idx || !out_score || !out_idx) return HHFM_EINVAL;
+  launch_merge(in_score, in_idx, R, B, K, /*stride_r=*/B * K, /*stride_b=*/K,
+               out_score, out_idx, reinterpret_cast<hipStream_t>(stream));
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,61 @@
+// Shared device helpers for the gfx950 FM-family kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hhfm.h"
+
+#define HHFM_DEV __device__ __forceinline__
+
+namespace hhfm {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// 16-byte chunk of an embedding row, widened to fp32.
+// fp32 rows: 4 elements per chunk; bf16 rows: 8 elements per chunk.
+template <bool BF16>
+struct Chunk;
+
+template <>
+struct Chunk<false> {
+  static constexpr int kElems = 4;
+  float v[4];
+  HHFM_DEV void load(const void* p) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+};
+
+template <>
+struct Chunk<true> {
+  static constexpr int kElems = 8;
+  float v[8];
+  HHFM_DEV void load(const void* p) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);             // low bf16
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);  // high bf16
+    }
+  }
+};
+
+HHFM_DEV float bf16_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
+
+// Out-of-range ids are clamped to row 0 so a bad index can never fault the
+// device; the Python layer validates ids and raises (TF embedding_lookup
+// raises InvalidArgumentError on them).
+HHFM_DEV int32_t clamp_id(int32_t id, int64_t M) {
+  return (uint64_t)(uint32_t)id < (uint64_t)M ? id : 0;
+}
+
+// Butterfly sum over aligned groups of G lanes (G a power of two <= 64).
+template <int G>
+HHFM_DEV float group_sum(float x) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, kWave);
+  return x;
+}
+
+}  // namespace hhfm

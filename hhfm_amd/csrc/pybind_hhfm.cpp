@@ -1,0 +1,119 @@
+// Thin pybind11 binding of the C ABI in include/hhfm.h.
+// Takes raw device pointers / hipStream_t handles as integers (the Python
+// layer passes tensor.data_ptr() and torch.cuda.current_stream().cuda_stream),
+// releases the GIL around every launch and turns a non-zero status into an
+// exception.  No torch types cross this boundary.
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "hhfm.h"
+
+namespace py = pybind11;
+using uptr = std::uintptr_t;
+
+template <typename T>
+static T* P(uptr p) { return reinterpret_cast<T*>(p); }
+
+static void check(int rc, const char* what) {
+  if (rc == HHFM_OK) return;
+  std::string msg = std::string(what) + ": " + hhfm_error_string(rc) +
+                    " (code " + std::to_string(rc) + ")";
+  if (rc == HHFM_EINVAL || rc == HHFM_EUNSUPPORTED || rc == HHFM_EWORKSPACE)
+    throw py::value_error(msg);
+  throw std::runtime_error(msg);
+}
+
+PYBIND11_MODULE(_hhfm, m) {
+  m.doc() = "pybind11 binding of libhhfm (MI355X FM-family scoring kernels)";
+  m.attr("ABI_VERSION") = HHFM_ABI_VERSION;
+  m.attr("F32") = (int)HHFM_F32;
+  m.attr("BF16") = (int)HHFM_BF16;
+  m.attr("MODE_FM") = (int)HHFM_MODE_FM;
+  m.attr("MODE_HHFM") = (int)HHFM_MODE_HHFM;
+
+  m.def("abi_version", [] { return hhfm_abi_version(); });
+
+  m.def("fm_score_rows",
+        [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype,
+           uptr w, float w0, uptr out, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_fm_score_rows(P<const int32_t>(idx), B, F, P<const void>(E),
+                                    M, k, dtype, P<const float>(w), w0,
+                                    P<float>(out), P<void>(stream));
+          }
+          check(rc, "hhfm_fm_score_rows");
+        });
+
+  m.def("hybrid_score_rows",
+        [](uptr idx, int64_t B, int ncols, int ucol, int icol, int c0, int c1,
+           int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr out,
+           uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_hybrid_score_rows(P<const int32_t>(idx), B, ncols, ucol,
+                                        icol, c0, c1, t0, t1, P<const void>(E),
+                                        M, k, dtype, P<float>(out),
+                                        P<void>(stream));
+          }
+          check(rc, "hhfm_hybrid_score_rows");
+        });
+
+  m.def("catalog_topk_workspace",
+        [](int64_t B, int item_count, int k, int K) {
+          size_t ws = 0;
+          check(hhfm_catalog_topk_workspace(B, item_count, k, K, &ws),
+                "hhfm_catalog_topk_workspace");
+          return ws;
+        });
+
+  m.def("catalog_topk",
+        [](uptr qidx, int64_t B, int ncols, int mode, int ucol, int c0, int c1,
+           int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr w,
+           int item_row_begin, int item_count, int global_item_base, int K,
+           uptr top_score, uptr top_idx, uptr ws, size_t ws_bytes,
+           uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_catalog_topk(
+                P<const int32_t>(qidx), B, ncols, mode, ucol, c0, c1, t0, t1,
+                P<const void>(E), M, k, dtype, P<const float>(w),
+                item_row_begin, item_count, global_item_base, K,
+                P<float>(top_score), P<int32_t>(top_idx), P<void>(ws), ws_bytes,
+                P<void>(stream));
+          }
+          check(rc, "hhfm_catalog_topk");
+        });
+
+  m.def("topk_merge",
+        [](uptr in_score, uptr in_idx, int R, int64_t B, int K, uptr out_score,
+           uptr out_idx, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_topk_merge(P<const float>(in_score), P<const int32_t>(in_idx),
+                                 R, B, K, P<float>(out_score), P<int32_t>(out_idx),
+                                 P<void>(stream));
+          }
+          check(rc, "hhfm_topk_merge");
+        });
+
+  m.def("topk_merge_host",
+        [](uptr in_score, uptr in_idx, int R, int64_t B, int K, uptr out_score,
+           uptr out_idx) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_topk_merge_host(P<const float>(in_score),
+                                      P<const int32_t>(in_idx), R, B, K,
+                                      P<float>(out_score), P<int32_t>(out_idx));
+          }
+          check(rc, "hhfm_topk_merge_host");
+        });
+}

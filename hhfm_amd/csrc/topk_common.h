@@ -1,0 +1,77 @@
+// Wave-level top-K primitives (64-lane CDNA wavefronts).
+//
+// A top-K list lives one entry per lane (lanes [0, KPAD)), sorted by the
+// tf.nn.top_k order: score descending, index ascending on equal scores
+// (FM.py:185 / OurModel7.py:295 fetch tf.nn.top_k(score, 20)).
+#pragma once
+#include "hhfm_common.h"
+
+namespace hhfm {
+
+constexpr float kNegInf = -__builtin_huge_valf();
+constexpr int32_t kNoIdx = 0x7fffffff;
+
+// strict total order used everywhere: a ranks before b
+HHFM_DEV bool better(float as, int32_t ai, float bs, int32_t bi) {
+  return as > bs || (as == bs && ai < bi);
+}
+
+HHFM_DEV int lane_id() { return threadIdx.x & (kWave - 1); }
+
+HHFM_DEV float shfl_f(float v, int src) { return __shfl(v, src, kWave); }
+HHFM_DEV int32_t shfl_i(int32_t v, int src) { return __shfl(v, src, kWave); }
+
+// One compare-exchange step of a bitonic network: keep the better of
+// (self, lane^d) when keep_better, else the worse.
+HHFM_DEV void cx(float& s, int32_t& i, int d, bool keep_better) {
+  const int l = lane_id();
+  const float ps = __shfl_xor(s, d, kWave);
+  const int32_t pi = __shfl_xor(i, d, kWave);
+  const bool pb = better(ps, pi, s, i);
+  const bool take = keep_better ? pb : !pb;
+  (void)l;
+  s = take ? ps : s;
+  i = take ? pi : i;
+}
+
+// Bitonic sort, descending (best first), independently inside every aligned
+// group of N lanes (N power of two <= 64).
+template <int N>
+HHFM_DEV void bitonic_sort_desc(float& s, int32_t& i) {
+  const int l = lane_id() & (N - 1);
+#pragma unroll
+  for (int size = 2; size <= N; size <<= 1) {
+    const bool desc = (l & size) == 0 || size == N;
+#pragma unroll
+    for (int d = size >> 1; d >= 1; d >>= 1) {
+      const bool lower = (l & d) == 0;
+      cx(s, i, d, lower == desc);
+    }
+  }
+}
+
+// Sort a bitonic sequence held in aligned groups of N lanes, descending.
+template <int N>
+HHFM_DEV void bitonic_merge_desc(float& s, int32_t& i) {
+  const int l = lane_id() & (N - 1);
+#pragma unroll
+  for (int d = N >> 1; d >= 1; d >>= 1) cx(s, i, d, (l & d) == 0);
+}
+
+// Top-KPAD of the union of two descending lists A (self, lanes [0,KPAD)) and
+// B (lanes [0,KPAD) of bs/bi): elementwise best of A[l] and B[KPAD-1-l] is
+// bitonic and holds exactly the KPAD best; the merge network sorts it.
+template <int KPAD>
+HHFM_DEV void merge_lists(float& as, int32_t& ai, float bs, int32_t bi) {
+  const int l = lane_id();
+  const int src = (l < KPAD) ? (KPAD - 1 - l) : l;
+  const float rs = shfl_f(bs, src);
+  const int32_t ri = shfl_i(bi, src);
+  if (better(rs, ri, as, ai)) {
+    as = rs;
+    ai = ri;
+  }
+  bitonic_merge_desc<KPAD>(as, ai);
+}
+
+}  // namespace hhfm

@@ -1,0 +1,156 @@
+"""Tensor-level entry points over the C ABI (include/hhfm.h).
+
+PyTorch-ROCm is plumbing here: it owns device memory and streams.  Every
+function launches a hand-written gfx950 kernel from ``libhhfm.so`` on
+``torch.cuda.current_stream()``; there is no eager-PyTorch or CPU fallback.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from ._native import native
+
+MODE_FM = 0
+MODE_HHFM = 1
+
+
+def _dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return 0
+    if t.dtype == torch.bfloat16:
+        return 1
+    raise TypeError(f"embedding table must be float32 or bfloat16, got {t.dtype}")
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _need_cuda(*ts: Optional[torch.Tensor]) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("hhfm_amd kernels take device (cuda/HIP) tensors")
+        if not t.is_contiguous():
+            raise ValueError("hhfm_amd kernels take contiguous tensors")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError("all tensors must be on the same device")
+    return dev
+
+
+def _idx(t: torch.Tensor, name: str) -> torch.Tensor:
+    if t.dtype != torch.int32:
+        raise TypeError(f"{name} must be int32 (the reference feeds int32 placeholders)")
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D [rows, cols]")
+    return t
+
+
+def validate_ids(idx: torch.Tensor, features_M: int) -> None:
+    """Raise like tf.nn.embedding_lookup does for ids outside [0, M).
+    (The kernels clamp such ids to row 0 so they can never fault.)"""
+    if idx.numel() == 0:
+        return
+    lo, hi = int(idx.min()), int(idx.max())
+    if lo < 0 or hi >= features_M:
+        raise ValueError(f"indices must be in [0, {features_M}), got [{lo}, {hi}]")
+
+
+def fm_score_rows(idx: torch.Tensor, E: torch.Tensor, w: Optional[torch.Tensor],
+                  w0: float = 0.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """FM.out (FM.py:99-120) for rows ``idx`` [B, F] -> float32 [B]."""
+    _idx(idx, "idx")
+    dev = _need_cuda(idx, E, w, out)
+    B, F = idx.shape
+    M, k = E.shape
+    if w is not None and (w.dtype != torch.float32 or w.numel() != M):
+        raise ValueError("w must be float32 with features_M entries")
+    if out is None:
+        out = torch.empty(B, dtype=torch.float32, device=dev)
+    native().fm_score_rows(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E),
+                           0 if w is None else w.data_ptr(), float(w0),
+                           out.data_ptr(), _stream(dev))
+    return out
+
+
+def hybrid_score_rows(idx: torch.Tensor, E: torch.Tensor, user_col: int = 0,
+                      item_col: int = 1, ctx: Tuple[int, int] = (0, 0),
+                      time: Tuple[int, int] = (0, 0),
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """OUR.PositiveFeadback (OurModel7.py:105-171) for rows ``idx`` -> [B]."""
+    _idx(idx, "idx")
+    dev = _need_cuda(idx, E, out)
+    B, ncols = idx.shape
+    M, k = E.shape
+    if out is None:
+        out = torch.empty(B, dtype=torch.float32, device=dev)
+    native().hybrid_score_rows(idx.data_ptr(), B, ncols, user_col, item_col,
+                               ctx[0], ctx[1], time[0], time[1], E.data_ptr(), M, k,
+                               _dtype_code(E), out.data_ptr(), _stream(dev))
+    return out
+
+
+_WS = {}
+
+
+def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
+    key = (dev.index, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=dev)
+        _WS[key] = buf
+    return buf
+
+
+def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
+                 item_row_begin: int, item_count: int, global_item_base: int = 0,
+                 w: Optional[torch.Tensor] = None, user_col: int = 0,
+                 ctx: Tuple[int, int] = (0, 0), time: Tuple[int, int] = (0, 0)
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Full-catalog score + top-K (FM.topk FM.py:172-198, OUR.topk
+    OurModel7.py:229-307). Returns (scores float32 [B,K], ids int32 [B,K])."""
+    _idx(qidx, "qidx")
+    dev = _need_cuda(qidx, E, w)
+    B, ncols = qidx.shape
+    M, k = E.shape
+    nat = native()
+    ws_bytes = nat.catalog_topk_workspace(B, item_count, k, K)
+    ws = _workspace(dev, ws_bytes)
+    top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
+    top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
+    nat.catalog_topk(qidx.data_ptr(), B, ncols, mode, user_col, ctx[0], ctx[1],
+                     time[0], time[1], E.data_ptr(), M, k, _dtype_code(E),
+                     0 if w is None else w.data_ptr(), item_row_begin, item_count,
+                     global_item_base, K, top_s.data_ptr(), top_i.data_ptr(),
+                     ws.data_ptr(), ws.numel(), _stream(dev))
+    return top_s, top_i
+
+
+def topk_merge(scores: torch.Tensor, ids: torch.Tensor
+               ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Merge R sorted [B,K] lists (stacked [R,B,K], rank-major) into [B,K].
+    Device tensors use the HIP kernel; host tensors the C++ host merge."""
+    if scores.dim() != 3 or scores.shape != ids.shape:
+        raise ValueError("expected scores/ids of shape [R, B, K]")
+    if scores.dtype != torch.float32 or ids.dtype != torch.int32:
+        raise TypeError("scores float32, ids int32")
+    scores = scores.contiguous()
+    ids = ids.contiguous()
+    R, B, K = scores.shape
+    out_s = torch.empty(B, K, dtype=torch.float32, device=scores.device)
+    out_i = torch.empty(B, K, dtype=torch.int32, device=scores.device)
+    nat = native()
+    if scores.is_cuda:
+        _need_cuda(scores, ids)
+        nat.topk_merge(scores.data_ptr(), ids.data_ptr(), R, B, K, out_s.data_ptr(),
+                       out_i.data_ptr(), _stream(scores.device))
+    else:
+        nat.topk_merge_host(scores.data_ptr(), ids.data_ptr(), R, B, K,
+                            out_s.data_ptr(), out_i.data_ptr())
+    return out_s, out_i

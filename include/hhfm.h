@@ -1,0 +1,123 @@
+/*
+ * hhfm.h — C ABI of the MI355X (gfx950) factorization-machine scoring backend.
+ *
+ * The reference (data-man-34/HHFM, Newcode/{FM,OurModel7,AFM,DFM}.py) has no native code and no FFI:
+ * its hot path is a chain of TensorFlow-1.x graph ops run through
+ * `model.sess.run(...)`.  Each entry point below replaces one such op chain
+ * (reference file:line cited per function).  The Python host package
+ * `hhfm_amd` binds these through the thin pybind11 module `_hhfm`; the ctypes
+ * stub a maintainer would add instead is in INTEGRATION.md.
+ *
+ * Conventions (every function):
+ *   - all array pointers are DEVICE memory owned by the caller; the library
+ *     allocates nothing and keeps no global mutable state (reentrant);
+ *   - `stream` is a hipStream_t (NULL = default stream); every call is
+ *     asynchronous on it;
+ *   - index arrays are row-major int32 [rows][ncols] (the reference feeds
+ *     int32 placeholders, FM.py:89);
+ *   - embedding tables are row-major [features_M][k] in `dtype`
+ *     (HHFM_F32 or HHFM_BF16; compute is always fp32);
+ *   - return 0 on success, a positive hipError_t on a launch error, or a
+ *     negative HHFM_E* code for invalid arguments (see hhfm_error_string).
+ */
+#ifndef HHFM_H_
+#define HHFM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HHFM_ABI_VERSION 1
+
+enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
+
+/* catalog scoring modes */
+enum hhfm_catalog_mode {
+  HHFM_MODE_FM = 0,   /* FM.topk:  (u+f)·(i+f) + w_i        FM.py:174-185      */
+  HHFM_MODE_HHFM = 1  /* OUR.topk: (u+Σctx[+Σtime])·i        OurModel7.py:232-295 */
+};
+
+enum hhfm_status {
+  HHFM_OK = 0,
+  HHFM_EINVAL = -1,       /* bad size / pointer / column range            */
+  HHFM_EUNSUPPORTED = -2, /* shape outside what the kernels implement     */
+  HHFM_EWORKSPACE = -3    /* workspace smaller than *_workspace() reports */
+};
+
+const char* hhfm_error_string(int code);
+int hhfm_abi_version(void);
+
+/* ------------------------------------------------------------------------
+ * M1 — FM per-row score (replaces the `FM.out` graph, FM.py:99-120)
+ *   out[b] = Σ_k ½[(Σ_f E[x_bf,k])² − Σ_f E[x_bf,k]²] + Σ_f w[x_bf] + w0
+ * idx: int32 [B][F]; w may be NULL (then Σw = 0, the DeepFM-interaction use).
+ * out: float [B].
+ * ---------------------------------------------------------------------- */
+int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
+                       const void* E, int64_t features_M, int32_t k,
+                       int32_t dtype, const float* w, float w0, float* out,
+                       void* stream);
+
+/* ------------------------------------------------------------------------
+ * H1 — HHFM per-row score (replaces `OUR.PositiveFeadback`,
+ * OurModel7.py:105-171 with sum pooling, :14-19)
+ *   h_b = E[x_b,user_col] + Σ_{c∈[ctx_begin,ctx_end)} E[x_bc]
+ *                         (+ Σ_{t∈[time_begin,time_end)} E[x_bt])
+ *   out[b] = Σ_k h_b,k · E[x_b,item_col],k
+ * An empty range (begin == end) disables that term. idx: int32 [B][ncols].
+ * ---------------------------------------------------------------------- */
+int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B, int32_t ncols,
+                           int32_t user_col, int32_t item_col,
+                           int32_t ctx_begin, int32_t ctx_end,
+                           int32_t time_begin, int32_t time_end,
+                           const void* E, int64_t features_M, int32_t k,
+                           int32_t dtype, float* out, void* stream);
+
+/* ------------------------------------------------------------------------
+ * M2/H2 — full-catalog score + fused top-K (replaces FM.topk, FM.py:172-198,
+ * and OUR.topk, OurModel7.py:229-307: broadcast multiply [B,N,k] +
+ * reduce_sum + tf.nn.top_k), without materialising the [B,N] score matrix.
+ *
+ *   query columns (qidx int32 [B][ncols]):
+ *     HHFM_MODE_HHFM: h = E[user] + Σ ctx cols (+ Σ time cols); score = h·E[item]
+ *     HHFM_MODE_FM:   f = Σ ctx cols, q = E[user]+f;
+ *                     score = q·(E[item]+f) + w[item]   (w may be NULL)
+ *   catalog: items are rows [item_row_begin, item_row_begin+item_count) of E.
+ *   output:  top_score/top_idx [B][K], sorted by (score desc, index asc) —
+ *            tf.nn.top_k order; top_idx = global_item_base + offset in range.
+ *   K must be in [1, 64] and <= item_count.
+ * Workspace: query `hhfm_catalog_topk_workspace` with the same sizes.
+ * ---------------------------------------------------------------------- */
+int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count, int32_t k,
+                                int32_t K, size_t* ws_bytes);
+
+int hhfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t ncols,
+                      int32_t mode, int32_t user_col, int32_t ctx_begin,
+                      int32_t ctx_end, int32_t time_begin, int32_t time_end,
+                      const void* E, int64_t features_M, int32_t k,
+                      int32_t dtype, const float* w, int32_t item_row_begin,
+                      int32_t item_count, int32_t global_item_base, int32_t K,
+                      float* top_score, int32_t* top_idx, void* workspace,
+                      size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Top-K merge of R sorted partial lists per query (the item-sharded
+ * multi-GPU path: RCCL all-gather output, rank-major).  Replaces the single
+ * tf.nn.top_k over the full catalog (FM.py:185, OurModel7.py:295).
+ *   in_score/in_idx: [R][B][K]; out_*: [B][K]; same (score desc, idx asc) order.
+ * hhfm_topk_merge_host is the same merge on host memory (no GPU needed).
+ * ---------------------------------------------------------------------- */
+int hhfm_topk_merge(const float* in_score, const int32_t* in_idx, int32_t R,
+                    int64_t B, int32_t K, float* out_score, int32_t* out_idx,
+                    void* stream);
+int hhfm_topk_merge_host(const float* in_score, const int32_t* in_idx,
+                         int32_t R, int64_t B, int32_t K, float* out_score,
+                         int32_t* out_idx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HHFM_H_ */

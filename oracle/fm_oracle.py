@@ -1,0 +1,193 @@
+"""CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+A numpy restatement, op for op, of the reference's TensorFlow-1.x scoring
+graphs (data-man-34/HHFM, Newcode/*.py).  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may use
+this module, and only as the checker: the product path (``hhfm_amd``) never
+imports it and fails loudly when its HIP extension is missing.
+
+Third-party dependency restated: TensorFlow 1.x (unpinned in the reference —
+no requirements file; ``Newcode/__pycache__`` is CPython 3.6 bytecode and the
+code uses ``tf.contrib``/``keep_dims``/``tf.Session``, i.e. TF 1.5–1.15).
+Ops restated with their published semantics: ``embedding_lookup`` (row
+gather), ``reduce_sum``/``reduce_max``, elementwise ``square``/``multiply``/
+``subtract``/``add_n``, ``matmul``, ``nn.relu``, ``nn.softmax``, ``exp``,
+``concat`` and ``nn.top_k`` (sorted=True: descending values, equal values
+keep the lower index first).  All arithmetic is float32 like the reference
+graphs; reductions are numpy's (TF's Eigen reduction order is not
+reproducible without TF — scores are compared with a tolerance, index sets
+exactly where the score gap exceeds it).
+
+Parity pinning: these functions are checked against golden vectors produced
+by running the reference's own model classes (``Newcode/FM.py``,
+``OurModel7.py``, ``AFM.py``, ``DFM.py``) on a numpy evaluation of the TF1
+ops (``tests/golden/make_golden.py``), see ``tests/test_oracle_golden.py``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+F32 = np.float32
+
+
+def _emb(E, ids):
+    """tf.nn.embedding_lookup: row gather (E stays float32)."""
+    return np.asarray(E, dtype=F32)[np.asarray(ids, dtype=np.int64)]
+
+
+def top_k(score: np.ndarray, k: int):
+    """tf.nn.top_k(score, k) on the last axis: values and indices sorted by
+    value descending; ties broken by lower index first (stable sort)."""
+    score = np.asarray(score, dtype=F32)
+    order = np.argsort(-score, axis=-1, kind="stable")[..., :k]
+    return np.take_along_axis(score, order, axis=-1), order.astype(np.int32)
+
+
+# ---------------------------------------------------------------------------
+# M1 — FM.out  (Newcode/FM.py:99-120)
+# ---------------------------------------------------------------------------
+def fm_out(X, E, w, w0=0.0):
+    """out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0, shape [B,1].
+
+    FM.py:99   nonzero_embeddings = embedding_lookup(E, X)        [B,F,k]
+    FM.py:100  summed = reduce_sum(., 1, keep_dims)               [B,1,k]
+    FM.py:102  summed_square = square(summed)
+    FM.py:105  squared = square(nonzero_embeddings)
+    FM.py:106  squared_sum = reduce_sum(squared, 1, keep_dims)
+    FM.py:109  FM = 0.5 * (summed_square - squared_sum)
+    FM.py:113  FM_OUT = reduce_sum(FM, 1)                         [B,k]
+    FM.py:114  dropout(keep=1) -> identity; batch_norm=0 (:111) -> skipped
+    FM.py:117  Bilinear = reduce_sum(FM_OUT, 1, keep_dims)        [B,1]
+    FM.py:118  Feature_bias = reduce_sum(embedding_lookup(w, X), 1)
+    FM.py:119  Bias = w0 * ones_like(labels)
+    FM.py:120  out = add_n([Bilinear, Feature_bias, Bias])
+    """
+    e = _emb(E, X)
+    summed = e.sum(axis=1, keepdims=True, dtype=F32)
+    sq_sum = np.square(e).sum(axis=1, keepdims=True, dtype=F32)
+    fm = F32(0.5) * (np.square(summed) - sq_sum)
+    fm_out_ = fm.sum(axis=1, dtype=F32)
+    bil = fm_out_.sum(axis=1, keepdims=True, dtype=F32)
+    if w is None:
+        fb = np.zeros_like(bil)
+    else:
+        fb = _emb(np.asarray(w, F32).reshape(-1, 1), X).sum(axis=1, dtype=F32)
+    return (bil + fb) + F32(w0)
+
+
+# ---------------------------------------------------------------------------
+# M2 — FM.topk  (Newcode/FM.py:172-198)
+# ---------------------------------------------------------------------------
+def fm_catalog_scores(A, E, w, n_user, n_item):
+    """bias + score, shape [B, n_item] (FM.py:174-184).
+
+    FM.py:174  user = lookup(E, A[:,0])
+    FM.py:175  item = lookup(E, n_user .. n_user+n_item-1)
+    FM.py:176  feature = reduce_sum(lookup(E, A[:,2:]), axis=1)
+    FM.py:177  UserWithFeature = user + feature
+    FM.py:178  ItemWithFeature = item[None] + feature[:,None]
+    FM.py:180  mul = UserWithFeature[:,None] * ItemWithFeature
+    FM.py:183  score = reduce_sum(mul, 2)
+    FM.py:184  bias = transpose(lookup(w, items))   [1,N]
+    FM.py:185  top_k(bias + score, tp)
+    """
+    A = np.asarray(A)
+    user = _emb(E, A[:, 0])
+    item = _emb(E, np.arange(n_user, n_user + n_item))
+    feature = _emb(E, A[:, 2:]).sum(axis=1, dtype=F32)
+    uwf = user + feature
+    iwf = item[None, :, :] + feature[:, None, :]
+    score = (uwf[:, None, :] * iwf).sum(axis=2, dtype=F32)
+    if w is None:
+        return score
+    bias = np.asarray(w, F32).reshape(-1)[n_user:n_user + n_item][None, :]
+    return bias + score
+
+
+def fm_topk(A, E, w, n_user, n_item, tp=20):
+    return top_k(fm_catalog_scores(A, E, w, n_user, n_item), tp)
+
+
+# ---------------------------------------------------------------------------
+# H1/H2 — HHFM (OurModel7), sum pooling (OurModel7.py:14-19)
+# ---------------------------------------------------------------------------
+def _hybrid(E, user_ids, ctx_ids=None, time_ids=None):
+    """Σ over stack[user, Σctx, (Σtime)] (OurModel7.py:122-168, 244-292)."""
+    stack = [_emb(E, user_ids)]
+    if ctx_ids is not None:
+        stack.append(_emb(E, ctx_ids).sum(axis=1, dtype=F32))   # :124 / :255
+    if time_ids is not None:
+        stack.append(_emb(E, time_ids).sum(axis=1, dtype=F32))  # :141 / :267
+    out = stack[0]
+    for s in stack[1:]:
+        out = out + s                                            # :168 / :292
+    return out
+
+
+def hhfm_split(X, feature_dimension, time_dimension, context=True, time=False):
+    """The reference's column split of a row [user, item, ctx..., time...]
+    (partial_fit feeds, OurModel7.py:374-385; topk, :236-242)."""
+    X = np.asarray(X)
+    ctx = tim = None
+    if context and time:
+        ctx = X[:, 2:-time_dimension]
+        tim = X[:, -time_dimension:]
+    elif context:
+        ctx = X[:, 2:]
+    elif time:
+        tim = X[:, 2:]
+    return ctx, tim
+
+
+def hhfm_positive_feedback(X, E, feature_dimension, time_dimension,
+                           context=True, time=False):
+    """PositiveFeadback = reduce_sum(hybrid * E[item], 1, keep_dims) [B,1]
+    (OurModel7.py:171)."""
+    X = np.asarray(X)
+    ctx, tim = hhfm_split(X, feature_dimension, time_dimension, context, time)
+    h = _hybrid(E, X[:, 0], ctx, tim)
+    it = _emb(E, X[:, 1])
+    return (h * it).sum(axis=1, keepdims=True, dtype=F32)
+
+
+def hhfm_catalog_scores(A, E, n_user, n_item, feature_dimension,
+                        time_dimension, context=True, time=False):
+    """score = reduce_sum(hybrid[:,None] * items[None], 2) (OurModel7.py:294)."""
+    A = np.asarray(A)
+    ctx, tim = hhfm_split(A, feature_dimension, time_dimension, context, time)
+    h = _hybrid(E, A[:, 0], ctx, tim)
+    item = _emb(E, np.arange(n_user, n_user + n_item))
+    return (h[:, None, :] * item[None, :, :]).sum(axis=2, dtype=F32)
+
+
+def hhfm_topk(A, E, n_user, n_item, feature_dimension, time_dimension,
+              context=True, time=False, tp=20):
+    return top_k(hhfm_catalog_scores(A, E, n_user, n_item, feature_dimension,
+                                     time_dimension, context, time), tp)
+
+
+# ---------------------------------------------------------------------------
+# helpers for comparing GPU results with the oracle
+# ---------------------------------------------------------------------------
+def topk_index_agreement(ref_scores_sorted, ref_idx, got_idx, tol):
+    """Compare top-K index lists where the reference ranking is unambiguous.
+
+    Position p of a query is *decidable* when the score gaps on both sides of
+    p in the reference ordering exceed ``tol`` (ties and near-ties may be
+    legally reordered by a different fp32 summation order).  Returns
+    (n_mismatch_decidable, n_ambiguous)."""
+    ref_scores_sorted = np.asarray(ref_scores_sorted)
+    ref_idx = np.asarray(ref_idx)
+    got_idx = np.asarray(got_idx)
+    B, K = ref_idx.shape
+    mism = amb = 0
+    for b in range(B):
+        s = ref_scores_sorted[b]
+        for p in range(K):
+            lo = abs(s[p] - s[p + 1]) if p + 1 < len(s) else np.inf
+            hi = abs(s[p - 1] - s[p]) if p > 0 else np.inf
+            if min(lo, hi) <= tol:
+                amb += 1
+            elif ref_idx[b, p] != got_idx[b, p]:
+                mism += 1
+    return mism, amb

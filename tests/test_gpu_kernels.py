@@ -1,0 +1,197 @@
+"""GPU parity of the C-ABI kernels against the CPU oracle (seeded inputs).
+
+Tolerance (north_star: fp32 scores within 1e-5 relative): a score may differ
+from the oracle by 1e-5 x its natural magnitude (Σ|terms| of the reduction),
+since the reference's own TF reduction order is not reproducible.  Top-K
+index lists must match exactly at every position whose reference score is
+separated from its neighbours by more than that tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fm_oracle as orc
+from tests.helpers import bf16_round, synth_rows, table
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def _dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def _fm_scale(X, E, w, w0):
+    e = E[X.astype(np.int64)].astype(np.float64)
+    s = e.sum(1)
+    q = (e * e).sum(1)
+    scale = (0.5 * (s * s + q)).sum(1)
+    if w is not None:
+        scale += np.abs(w[X.astype(np.int64)]).sum(1)
+    return scale + abs(w0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k", [16, 32, 64, 128])
+@pytest.mark.parametrize("F", [2, 3, 5, 8, 12])
+def test_fm_score_rows_parity(dtype, k, F):
+    from hhfm_amd import ops
+    rng = np.random.default_rng(1000 + 7 * k + F)
+    B = 4099
+    M = 5051
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    E = table(rng, M, k)
+    w = rng.normal(0, 0.01, size=M).astype(np.float32)
+    w0 = 0.003
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    got = ops.fm_score_rows(_dev(X), Eg, _dev(w), w0).cpu().numpy()
+    ref = orc.fm_out(X, E, w, w0)[:, 0]
+    scale = _fm_scale(X, E, w, w0)
+    assert np.all(np.abs(got - ref) <= RTOL * scale + 1e-12)
+
+
+@pytest.mark.parametrize("B", [0, 1, 7, 63, 1000])
+def test_fm_score_rows_ragged_and_generic(B):
+    """Odd B, and k=20 (not 16-B aligned rows -> generic kernel), no w."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(B + 5)
+    M, k, F = 300, 20, 5
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    E = table(rng, M, k)
+    got = ops.fm_score_rows(_dev(X), _dev(E), None, 0.5).cpu().numpy()
+    ref = orc.fm_out(X, E, None, 0.5)[:, 0] if B else np.zeros(0, np.float32)
+    assert got.shape == (B,)
+    if B:
+        assert np.all(np.abs(got - ref) <= RTOL * _fm_scale(X, E, None, 0.5))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("layout", ["frappe", "jiaju", "resturant", "user_item"])
+@pytest.mark.parametrize("k", [32, 64, 128])
+def test_hybrid_score_rows_parity(dtype, layout, k):
+    from hhfm_amd import ops
+    rng = np.random.default_rng(77 + k)
+    ctx, td = {"frappe": ((7, 2, 3), 0), "jiaju": ((4, 3, 5, 2, 6), 3),
+               "resturant": ((4, 3, 5, 2, 6), 5), "user_item": ((), 0)}[layout]
+    X, M = synth_rows(rng, 3001, 300, 900, ctx, time_fields=td)
+    E = table(rng, M, k)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    fd = len(ctx)
+    c = (2, 2 + fd) if fd else (0, 0)
+    t = (2 + fd, 2 + fd + td) if td else (0, 0)
+    got = ops.hybrid_score_rows(_dev(X), Eg, 0, 1, c, t).cpu().numpy()
+    ref = orc.hhfm_positive_feedback(X, E, fd, td, context=fd > 0, time=td > 0)[:, 0]
+    e = np.abs(E[X.astype(np.int64)].astype(np.float64))
+    scale = (e[:, [0] + list(range(2, X.shape[1]))].sum(1) * e[:, 1]).sum(1)
+    assert np.all(np.abs(got - ref) <= RTOL * scale + 1e-12)
+
+
+def _hhfm_scale(A, E, n_user, n_item):
+    """Per-query magnitude of h·item: max over items of Σ_k |h_k||i_k|."""
+    h = np.abs(orc._hybrid(E, A[:, 0], A[:, 2:]).astype(np.float64))
+    it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
+    return (h @ it.T).max(1, keepdims=True)
+
+
+def _check_topk(ref_scores_full, got_s, got_i, K, scale):
+    rs, ri = orc.top_k(ref_scores_full, K + 1)
+    tol = RTOL * scale
+    mism, amb = orc.topk_index_agreement(rs, ri[:, :K], got_i, tol)
+    assert mism == 0, f"{mism} decidable top-K positions differ (ambiguous {amb})"
+    # every returned score equals the oracle score of the returned item
+    picked = np.take_along_axis(ref_scores_full, got_i.astype(np.int64), axis=1)
+    assert np.all(np.abs(picked - got_s) <= tol)
+    # sorted (score desc, idx asc)
+    d = np.diff(got_s, axis=1)
+    assert np.all(d <= 0)
+    return amb
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k", [32, 64, 128])
+@pytest.mark.parametrize("K", [1, 5, 20, 33, 64])
+def test_catalog_topk_hhfm_parity(dtype, k, K):
+    from hhfm_amd import ops
+    rng = np.random.default_rng(2 + k + K)
+    n_user, n_item = 957, 4082
+    A, M = synth_rows(rng, 300, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, n_user, n_item, 0,
+                            None, 0, (2, 5), (0, 0))
+    ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
+    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, _hhfm_scale(A, E, n_user, n_item))
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k", [16, 64])
+def test_catalog_topk_fm_parity(dtype, k):
+    from hhfm_amd import ops
+    rng = np.random.default_rng(5 + k)
+    n_user, n_item = 957, 4082
+    A, M = synth_rows(rng, 257, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    w = rng.normal(0, 0.01, size=M).astype(np.float32)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_FM, 20, n_user, n_item, 0,
+                            _dev(w), 0, (2, 5), (0, 0))
+    ref = orc.fm_catalog_scores(A, E, w, n_user, n_item)
+    f = E[A[:, 2:].astype(np.int64)].sum(1)
+    q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
+    it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
+    scale = (q @ it.T + (q * np.abs(f)).sum(1, keepdims=True)).max(1, keepdims=True) + 0.05
+    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
+
+
+def test_catalog_topk_large_catalog_shard_offsets():
+    """Many splits (merge path) + a shard with non-zero row/global base."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(3)
+    n_user, n_item, k = 1000, 60000, 64
+    A, M = synth_rows(rng, 200, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    shard_begin, shard_count = n_user + 20000, 25000
+    s, i = ops.catalog_topk(_dev(A), _dev(E), ops.MODE_HHFM, 20, shard_begin,
+                            shard_count, 20000, None, 0, (2, 5), (0, 0))
+    full = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
+    ref = np.full_like(full, -np.inf)
+    ref[:, 20000:45000] = full[:, 20000:45000]
+    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, _hhfm_scale(A, E, n_user, n_item))
+
+
+def test_catalog_topk_ties_lower_index_first():
+    """Identical item rows -> equal scores -> tf.nn.top_k keeps lower ids."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(11)
+    n_user, n_item, k = 10, 3000, 32
+    A, M = synth_rows(rng, 40, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    E[n_user:n_user + n_item] = E[n_user + 5]          # every item identical
+    s, i = ops.catalog_topk(_dev(A), _dev(E), ops.MODE_HHFM, 20, n_user, n_item, 0,
+                            None, 0, (2, 5), (0, 0))
+    assert np.array_equal(i.cpu().numpy(), np.tile(np.arange(20, dtype=np.int32), (40, 1)))
+
+
+def test_topk_merge_device_matches_host():
+    from hhfm_amd import ops
+    rng = np.random.default_rng(4)
+    R, B, K = 8, 333, 20
+    sc = rng.normal(size=(R, B, K)).astype(np.float32)
+    sc[:, :, 5] = sc[:, :, 4]                          # ties inside lists
+    sc[1] = sc[0]                                      # ties across lists
+    ids = rng.integers(0, 10**6, size=(R, B, K)).astype(np.int32)
+    order = np.lexsort((ids, -sc), axis=2)             # (score desc, idx asc)
+    sc = np.take_along_axis(sc, order, 2)
+    ids = np.take_along_axis(ids, order, 2)
+    hs, hi = ops.topk_merge(torch.from_numpy(sc), torch.from_numpy(ids))
+    ds, di = ops.topk_merge(_dev(sc), _dev(ids))
+    assert np.array_equal(hs.numpy(), ds.cpu().numpy())
+    assert np.array_equal(hi.numpy(), di.cpu().numpy())
