@@ -72,15 +72,23 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
         c[u][f].load(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
+    // Σ_f w[x_f]: lane `sub` gathers fields f ≡ sub (mod LPR); loads are
+    // unconditional (clamped ids) so the vmcnt counting stays exact
     float wv[U];
     if constexpr (HAS_W) {
+      constexpr int WPL = (F + LPR - 1) / LPR;
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        int32_t my = id[u][0];
+        wv[u] = 0.f;
 #pragma unroll
-        for (int f = 1; f < F; ++f) my = (sub == f) ? id[u][f] : my;
-        const float wl = w[my];  // unconditional: keeps vmcnt counting exact
-        wv[u] = (sub < F) ? wl : 0.f;
+        for (int r = 0; r < WPL; ++r) {
+          const int fsel = r * LPR + sub;
+          int32_t my = id[u][0];
+#pragma unroll
+          for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
+          const float wl = w[my];
+          wv[u] += (fsel < F) ? wl : 0.f;
+        }
       }
     }
 

@@ -1,0 +1,115 @@
+"""Item-sharded full-catalog top-K across the GPUs of a node.
+
+The reference ranks the whole catalog on one device with one tf.nn.top_k
+(FM.py:185, OurModel7.py:295).  Here, one process per GPU:
+  1. rank r owns the contiguous item range [begin_r, end_r) of the catalog
+     (tables are replicated: users + ctx are tiny, items are read only in
+     the rank's range);
+  2. it computes its local top-K with hhfm_catalog_topk (scores fp32, ids
+     already global item offsets);
+  3. one all-gather of (score, id) [B, K] per rank — RCCL over xGMI when the
+     process group is ``nccl``, gloo on CPU;
+  4. hhfm_topk_merge (device) / hhfm_topk_merge_host merges the R sorted
+     lists with the same (score desc, id asc) order, which reproduces the
+     single-device ranking because ranges are contiguous and ordered.
+Payload per rank: B*K*8 bytes (160 KB at B=1024, K=20) — latency-bound.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+NEG_INF = float("-inf")
+NO_IDX = 0x7FFFFFFF
+
+
+def shard_range(n_item: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous near-equal split (first n_item % world ranks get one more)."""
+    base, extra = divmod(n_item, world)
+    begin = rank * base + min(rank, extra)
+    return begin, begin + base + (1 if rank < extra else 0)
+
+
+def _pad(scores: torch.Tensor, ids: torch.Tensor, K: int):
+    if scores.shape[1] == K:
+        return scores, ids
+    B = scores.shape[0]
+    ps = torch.full((B, K), NEG_INF, dtype=torch.float32, device=scores.device)
+    pi = torch.full((B, K), NO_IDX, dtype=torch.int32, device=ids.device)
+    ps[:, :scores.shape[1]] = scores
+    pi[:, :ids.shape[1]] = ids
+    return ps, pi
+
+
+def gather_topk(scores: torch.Tensor, ids: torch.Tensor, group=None):
+    """All-gather each rank's [B,K] lists -> [R,B,K] (rank-major)."""
+    world = dist.get_world_size(group)
+    B, K = scores.shape
+    out_s = torch.empty(world, B, K, dtype=scores.dtype, device=scores.device)
+    out_i = torch.empty(world, B, K, dtype=ids.dtype, device=ids.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out_s, scores.contiguous(), group=group)
+        dist.all_gather_into_tensor(out_i, ids.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out_s.unbind(0)), scores.contiguous(), group=group)
+        dist.all_gather(list(out_i.unbind(0)), ids.contiguous(), group=group)
+    return out_s, out_i
+
+
+LocalScorer = Callable[[object, int, int, int], Tuple[torch.Tensor, torch.Tensor]]
+
+
+def sharded_topk(A, K: int, n_item: int, local_scorer: LocalScorer, group=None):
+    """Global top-K over an item-sharded catalog.
+
+    ``local_scorer(A, begin, count, K_local)`` returns this rank's sorted
+    (scores float32 [B,K_local], global item ids int32 [B,K_local]) for items
+    [begin, begin+count); the product scorer is ``model_scorer(model)``.
+    """
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if K > n_item:
+        raise ValueError(f"K={K} exceeds the catalog size {n_item}")
+    begin, end = shard_range(n_item, world, rank)
+    count = end - begin
+    if count > 0:
+        s, i = local_scorer(A, begin, count, min(K, count))
+        s, i = _pad(s, i, K)
+    else:
+        B = len(A)
+        dev = torch.device("cuda", torch.cuda.current_device()) if \
+            dist.is_initialized() and dist.get_backend(group) == "nccl" else torch.device("cpu")
+        s = torch.full((B, K), NEG_INF, dtype=torch.float32, device=dev)
+        i = torch.full((B, K), NO_IDX, dtype=torch.int32, device=dev)
+    if world == 1:
+        return s, i
+    gs, gi = gather_topk(s, i, group)
+    return ops.topk_merge(gs, gi)
+
+
+def model_scorer(model) -> LocalScorer:
+    """The HIP local scorer of an FM / OUR model for its rank's item range."""
+    def score(A, begin, count, K):
+        q = model._idx(A)
+        ncols = q.shape[1]
+        if hasattr(model, "_ranges"):      # OUR (HHFM) model
+            ctx, tim = model._ranges(ncols)
+            mode, w = ops.MODE_HHFM, None
+        else:
+            ctx, tim = ((2, ncols) if ncols > 2 else (0, 0)), (0, 0)
+            mode, w = ops.MODE_FM, model.weights["feature_bias"].reshape(-1)
+        return ops.catalog_topk(q, model.table, mode, K, model.n_user + begin, count, begin,
+                                w, 0, ctx, tim)
+    return score
+
+
+def sharded_model_topk(model, A, tp, group=None) -> np.ndarray:
+    """Drop-in for ``model.topk(A, tp)`` with the catalog sharded over the
+    ranks of ``group`` (every rank calls it with the same A)."""
+    _, ids = sharded_topk(A, int(tp), model.n_item, model_scorer(model), group)
+    return ids.cpu().numpy()

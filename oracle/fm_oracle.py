@@ -180,14 +180,96 @@ def topk_index_agreement(ref_scores_sorted, ref_idx, got_idx, tol):
     ref_idx = np.asarray(ref_idx)
     got_idx = np.asarray(got_idx)
     B, K = ref_idx.shape
+    tol = np.broadcast_to(np.asarray(tol, dtype=np.float64).reshape(-1, 1)
+                          if np.ndim(tol) else np.float64(tol), (B, 1))
     mism = amb = 0
     for b in range(B):
         s = ref_scores_sorted[b]
         for p in range(K):
             lo = abs(s[p] - s[p + 1]) if p + 1 < len(s) else np.inf
             hi = abs(s[p - 1] - s[p]) if p > 0 else np.inf
-            if min(lo, hi) <= tol:
+            if min(lo, hi) <= tol[b, 0]:
                 amb += 1
             elif ref_idx[b, p] != got_idx[b, p]:
                 mism += 1
     return mism, amb
+
+
+# ---------------------------------------------------------------------------
+# A1/A2 — AFM (Newcode/AFM.py)
+# ---------------------------------------------------------------------------
+def _pairs(e):
+    """element_wise_product_list over i<j (AFM.py:107-112) -> [B, P, k]."""
+    F = e.shape[1]
+    return np.stack([e[:, i, :] * e[:, j, :] for i in range(F) for j in range(i + 1, F)], 1)
+
+
+def _att_logit(p, W, b, pvec):
+    """Σ_A p * relu(reshape(p,[-1,k]) @ W + b)  (AFM.py:117-124, 221-224)."""
+    shp = p.shape
+    mul = np.matmul(p.reshape(-1, shp[-1]), W).astype(F32).reshape(*shp[:-1], W.shape[1])
+    return (np.asarray(pvec, F32) * np.maximum(mul + np.asarray(b, F32).reshape(-1), 0)).sum(
+        axis=-1, keepdims=True, dtype=F32)
+
+
+def afm_out(X, E, w, w0, W, b, pvec, P):
+    """AFM.out (AFM.py:103-142), attention=1, keep=[1,1] -> [B,1]."""
+    e = _emb(E, X)
+    pr = _pairs(e)                                           # [B,P,k]
+    logit = _att_logit(pr, W, b, pvec)                       # [B,P,1]
+    ex = np.exp(logit - logit.max(axis=1, keepdims=True))
+    att = (ex / ex.sum(axis=1, keepdims=True)).astype(F32)   # softmax axis=1 (:125)
+    afm = (att * pr).sum(axis=1, dtype=F32)                  # [B,k]      (:130)
+    bil = np.matmul(afm, np.asarray(P, F32)).sum(axis=1, keepdims=True, dtype=F32)  # :138-139
+    fb = _emb(np.asarray(w, F32).reshape(-1, 1), X).sum(axis=1, dtype=F32)          # :140
+    return (bil + fb) + F32(w0)                                                     # :142
+
+
+def afm_catalog_scores(A, E, w, W, b, pvec, P, n_user, n_item):
+    """score3 + bias of AFM.topk (AFM.py:210-243) -> [B, N]."""
+    A = np.asarray(A)
+    uf = np.concatenate([_emb(E, A[:, 0])[:, None, :], _emb(E, A[:, 2:])], axis=1)  # :210-212
+    ufp = _pairs(uf)                                                  # [B,C,k]  :214-220
+    a_uf = np.exp(_att_logit(ufp, W, b, pvec))                        # [B,C,1]  :221-224
+    item = _emb(E, np.arange(n_user, n_user + n_item))                # [N,k]    :226
+    ufi = uf[:, None, :, :] * item[None, :, None, :]                  # [B,N,uf,k] :227
+    a_ufi = np.exp(_att_logit(ufi, W, b, pvec))                       # [B,N,uf,1] :228-230
+    ufw = (ufp * a_uf).sum(axis=1, dtype=F32)                         # [B,k]    :232
+    iufw = (ufi * a_ufi).sum(axis=2, dtype=F32)                       # [B,N,k]  :233
+    s1 = ufw[:, None, :] + iufw                                       # :234
+    wt = a_uf.sum(axis=1, dtype=F32)[:, None, :] + a_ufi.sum(axis=2, dtype=F32)  # :235
+    s2 = s1 / wt                                                      # :236
+    s3 = (s2 * np.asarray(P, F32).T).sum(axis=2, dtype=F32)           # :239
+    bias = np.asarray(w, F32).reshape(-1)[n_user:n_user + n_item][None, :]  # :240
+    return s3 + bias                                                  # :243
+
+
+# ---------------------------------------------------------------------------
+# D1/D2 — DeepFM (Newcode/DFM.py)
+# ---------------------------------------------------------------------------
+def dfm_out(X, E, w, layers, biases, Wp, bp):
+    """DeepFM.out (DFM.py:104-137), use_fm = use_deep = True, loss 'mse'."""
+    X = np.asarray(X)
+    e = _emb(E, X)                                                    # :104
+    y1 = _emb(np.asarray(w, F32).reshape(-1, 1), X).sum(axis=2, dtype=F32)   # :109-110 [B,F]
+    s = e.sum(axis=1, dtype=F32)                                      # :114
+    y2 = F32(0.5) * (np.square(s) - np.square(e).sum(axis=1, dtype=F32))     # :115-122
+    y = e.reshape(-1, e.shape[1] * e.shape[2])                        # :125
+    for Wl, bl in zip(layers, biases):                                # :126-128 (relu on every layer)
+        y = np.maximum(np.matmul(y, np.asarray(Wl, F32)).astype(F32) + np.asarray(bl, F32), 0)
+    cat = np.concatenate([y1, y2, y], axis=1)                         # :132
+    return np.matmul(cat, np.asarray(Wp, F32)).astype(F32) + F32(bp)  # :137
+
+
+def dfm_catalog_rows(A, n_user, n_item):
+    """DeepFM.topk's candidate rows (DFM.py:220-223): each query tiled over all
+    items with column 1 replaced by the item id -> [B*N, F]."""
+    A = np.asarray(A, dtype=np.int64)
+    neg = np.repeat(A[:, None, :], n_item, axis=1)
+    neg[:, :, 1] = np.arange(n_user, n_user + n_item)[None, :]
+    return neg.reshape(-1, A.shape[1])
+
+
+def dfm_catalog_scores(A, E, w, layers, biases, Wp, bp, n_user, n_item):
+    rows = dfm_catalog_rows(A, n_user, n_item)
+    return dfm_out(rows, E, w, layers, biases, Wp, bp).reshape(-1, n_item)  # :228

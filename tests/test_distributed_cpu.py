@@ -1,0 +1,68 @@
+"""World-size-2 (and 3) gloo runs of the item-sharded top-K path: shard
+split, all-gather, host merge == single-device ranking.  The per-shard scorer
+is the C oracle here (no GPU); on the box the same code runs the HIP scorer
+and RCCL (tests/test_gpu_models.py)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hhfm_amd import distributed as hd
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import cpu as ocpu
+    from tests.helpers import synth_rows, table
+    rng = np.random.default_rng(42)
+    nu, ni = 300, 5000
+    A, M = synth_rows(rng, 64, nu, ni, (7, 2, 3))
+    E = table(rng, M, 32)
+    E[nu + 100] = E[nu + 4000]                  # a cross-shard exact tie
+
+    def scorer(A_, begin, count, K):
+        s, i = ocpu.catalog_topk(A_, E, 1, K, nu + begin, count, ctx=(2, 5), threads=1)
+        return torch.from_numpy(s), torch.from_numpy(i + begin)
+
+    s, i = hd.sharded_topk(A, 20, ni, scorer)
+    if rank == 0:
+        rs, ri = ocpu.catalog_topk(A, E, 1, 20, nu, ni, ctx=(2, 5), threads=1)
+        q.put((np.array_equal(i.numpy(), ri), float(np.abs(s.numpy() - rs).max())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_topk_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    same, err = q.get(timeout=10)
+    assert same and err == 0.0
+
+
+def test_shard_range_partition():
+    for n in [1, 7, 4082, 10_000_000]:
+        for w in [1, 2, 3, 8]:
+            rs = [hd.shard_range(n, w, r) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(e - b for b, e in rs) - min(e - b for b, e in rs) <= 1

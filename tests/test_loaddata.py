@@ -1,0 +1,85 @@
+"""hhfm_amd.NewLoadData.LoadData vs the reference LoadData's outputs
+(tests/golden/make_golden.py ran Newcode/NewLoadData.py with seed 2016)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from hhfm_amd.NewLoadData import LoadData
+
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("tag", ["frappe", "jiaju"])
+def test_loaddata_matches_reference(tag):
+    ref = np.load(os.path.join(G, f"loaddata_{tag}.npz"))
+    np.random.seed(2016)
+    d = LoadData(G + "/", f"synth_{tag}")
+    assert d.n_user == int(ref["n_user"]) and d.n_item == int(ref["n_item"])
+    assert d.features_M == int(ref["features_M"])
+    assert list(d.Train_data.columns) == list(ref["columns"])
+    assert np.array_equal(d.Train_data.values, ref["train"])
+    assert np.array_equal(d.Test_data.values, ref["test"])
+    keys, items = [], []
+    for k in sorted(d.positive_feedback):
+        for it in sorted(d.positive_feedback[k]):
+            keys.append(k)
+            items.append(it)
+    assert np.array_equal(np.array(keys), ref["pf_keys"])
+    assert np.array_equal(np.array(items), ref["pf_items"])
+
+
+def test_loaddata_shared_token_ids():
+    """Quirk 1: identical tokens in different columns share one id."""
+    np.random.seed(0)
+    d = LoadData(G + "/", "synth_frappe")
+    import pandas as pd
+    raw = pd.read_csv(os.path.join(G, "synth_frappe", "synth_frappe.libfm"), sep=" ", header=None)
+    tokens = raw.values[:, 1:].T.reshape(-1)
+    first = {}
+    for t in tokens:
+        first.setdefault(t, len(first))
+    assert d.features_M == len(first)
+    # "night" appears as daytime and as homework value -> one id
+    assert "night" in set(raw[3]) and "night" in set(raw[5])
+
+
+REAL = "/root/reference/data/positive/"
+
+
+@pytest.mark.skipif(not os.path.exists(REAL + "frappe/frappe.libfm"),
+                    reason="real Frappe only exists in the builder container")
+def test_loaddata_real_frappe_hashes():
+    with open(os.path.join(G, "frappe_real.json")) as f:
+        ref = json.load(f)
+    np.random.seed(2016)
+    d = LoadData(REAL, "frappe")
+    assert [d.n_user, d.n_item, d.features_M] == ref["sizes"]
+    assert hashlib.sha256(np.ascontiguousarray(d.Train_data.values, np.int64)).hexdigest() == ref["train_sha256"]
+    assert hashlib.sha256(np.ascontiguousarray(d.Test_data.values, np.int64)).hexdigest() == ref["test_sha256"]
+
+
+@pytest.mark.skipif(not os.path.exists(REAL + "frappe/frappe.libfm"),
+                    reason="real Frappe only exists in the builder container")
+def test_hr_at_k_real_frappe_matches_reference_harness():
+    """Same loader split + same sampled rows + same top-20 lists => the same
+    HR/NDCG/PRE@K as the reference harness on real Frappe (model: seeded
+    random-weight HHFM scored by the oracle; trained reference weights do
+    not exist)."""
+    from hhfm_amd.OurModel7 import Train as M7Train
+    from tests.test_harness import OracleModel
+    with open(os.path.join(G, "frappe_real.json")) as f:
+        ref = json.load(f)
+    np.random.seed(2016)
+    d = LoadData(REAL, "frappe")
+    E = np.random.default_rng(606).normal(0, 0.01, (d.features_M, 64)).astype(np.float32)
+    m = OracleModel(E, None, d.n_user, d.n_item, fm_scores=False)
+    for topk in (5, 10):
+        t = M7Train.__new__(M7Train)
+        import hhfm_amd.harness as H
+        H.Train.__init__(t, data=d, model=m)
+        t.TopK = topk
+        np.random.seed(31)
+        assert t.evaluate_TopK(d.Test_data) == ref[f"hhfm_random_w_topk{topk}"]
