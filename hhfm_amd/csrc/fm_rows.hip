@@ -25,7 +25,7 @@ struct RowsPerLane {
 
 // Raw (unclamped) index rows: nothing may consume them until the gathers
 // issued before them are consumed, or the in-order vmcnt would serialise.
-template <int F, int U>
+template <int F, int U, bool NT = false>
 HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
                        int64_t base, int64_t B, int g, int RPW, int ncols) {
 #pragma unroll
@@ -33,14 +33,14 @@ HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
     int64_t row = base + (int64_t)u * RPW + g;
     const int32_t* p = idx + (row < B ? row : 0) * (int64_t)ncols;
 #pragma unroll
-    for (int f = 0; f < F; ++f) id[u][f] = p[f];
+    for (int f = 0; f < F; ++f) id[u][f] = load_i32<NT>(p + f);
   }
 }
 
 // ---------------------------------------------------------------------------
 // FM row kernel: out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0
 // ---------------------------------------------------------------------------
-template <int F, int LPR, bool BF16, bool HAS_W>
+template <int F, int LPR, bool BF16, bool HAS_W, bool NT>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
     int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out) {
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
 
   int64_t base = wave * RPI;
   int32_t raw[U][F];
-  if (base < B) load_ids<F, U>(raw, idx, base, B, g, RPW, F);
+  if (base < B) load_ids<F, U, NT>(raw, idx, base, B, g, RPW, F);
 
   for (; base < B; base += stride) {
     C c[U][F];
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
 #pragma unroll
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
-        c[u][f].load(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
+        c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
     // Σ_f w[x_f]: lane `sub` gathers fields f ≡ sub (mod LPR); loads are
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
 
     // prefetch next iteration's index rows before consuming the gathers
     // (unconditional: rows past B read row 0, which keeps vmcnt counting exact)
-    load_ids<F, U>(raw, idx, base + stride, B, g, RPW, F);
+    load_ids<F, U, NT>(raw, idx, base + stride, B, g, RPW, F);
 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -114,7 +114,10 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
       float fb = 0.f;
       if constexpr (HAS_W) fb = group_sum<LPR>(wv[u]);
       const int64_t row = base + (int64_t)u * RPW + g;
-      if (sub == 0 && row < B) out[row] = (t + fb) + w0;
+      if (sub == 0 && row < B) {
+        if constexpr (NT) __builtin_nontemporal_store((t + fb) + w0, out + row);
+        else out[row] = (t + fb) + w0;
+      }
     }
   }
 }
@@ -264,14 +267,17 @@ static int grid_for(int64_t rows, int64_t rows_per_block) {
 template <int F, int LPR, bool BF16>
 static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            int64_t M, const float* w, float w0, float* out,
-                           hipStream_t s) {
+                           bool nt, hipStream_t s) {
   constexpr int RPB = 4 * (kWave / LPR) * RowsPerLane<F>::value;
   const int grid = grid_for(B, RPB);
-  if (w)
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true>), dim3(grid), dim3(256),
-                       0, s, idx, B, E, M, w, w0, out);
+  if (w && nt)
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, true>), dim3(grid),
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out);
+  else if (w)
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, false>), dim3(grid),
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out);
   else
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false>), dim3(grid),
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, false>), dim3(grid),
                        dim3(256), 0, s, idx, B, E, M, w, w0, out);
 }
 
@@ -312,11 +318,11 @@ static void launch_hybrid_fast(const int32_t* idx, int64_t B, int nctx,
 
 static bool try_fm_fast(const int32_t* idx, int64_t B, int F, const char* E,
                         int64_t M, int lpr, bool bf16, const float* w, float w0,
-                        float* out, hipStream_t s) {
+                        float* out, bool nt, hipStream_t s) {
   if (bf16) {
-    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, s)
+    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, nt, s)
   } else {
-    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, s)
+    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, nt, s)
   }
   return true;
 }
@@ -342,10 +348,10 @@ static int lpr_for(int64_t k, int dtype) {
 
 using namespace hhfm;
 
-extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
-                                  const void* E, int64_t features_M, int32_t k,
-                                  int32_t dtype, const float* w, float w0,
-                                  float* out, void* stream) {
+extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
+                                     const void* E, int64_t features_M, int32_t k,
+                                     int32_t dtype, const float* w, float w0,
+                                     float* out, int32_t flags, void* stream) {
   if (B < 0 || F < 1 || F > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (B == 0) return HHFM_OK;
@@ -356,7 +362,7 @@ extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
   const bool aligned = (reinterpret_cast<uintptr_t>(E) & 15) == 0;
   if (!(lpr && aligned &&
         try_fm_fast(idx, B, F, reinterpret_cast<const char*>(E), features_M,
-                    lpr, bf16, w, w0, out, s))) {
+                    lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0, s))) {
     const int grid = grid_for(B, 4);
     if (bf16)
       hipLaunchKernelGGL(fm_rows_generic<true>, dim3(grid), dim3(256), 0, s, idx,
@@ -368,6 +374,14 @@ extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                          features_M, k, w, w0, out);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
+                                  const void* E, int64_t features_M, int32_t k,
+                                  int32_t dtype, const float* w, float w0,
+                                  float* out, void* stream) {
+  return hhfm_fm_score_rows_ex(idx, B, F, E, features_M, k, dtype, w, w0, out,
+                               HHFM_FM_ROWS_DEFAULT_FLAGS, stream);
 }
 
 extern "C" int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B,

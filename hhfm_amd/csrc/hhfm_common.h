@@ -11,6 +11,24 @@ namespace hhfm {
 
 constexpr int kWave = 64;  // CDNA wavefront
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-byte load; NT = non-temporal (streamed once: does not displace the
+// hot, re-read data — e.g. the FM bias table — from L2 / Infinity Cache)
+template <bool NT>
+HHFM_DEV u32x4_t load16(const void* p) {
+  const u32x4_t* q = reinterpret_cast<const u32x4_t*>(p);
+  if constexpr (NT) return __builtin_nontemporal_load(q);
+  else return *q;
+}
+
+template <bool NT>
+HHFM_DEV int32_t load_i32(const int32_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // 16-byte chunk of an embedding row, widened to fp32.
 // fp32 rows: 4 elements per chunk; bf16 rows: 8 elements per chunk.
 template <bool BF16>
@@ -20,9 +38,11 @@ template <>
 struct Chunk<false> {
   static constexpr int kElems = 4;
   float v[4];
+  template <bool NT = false>
   HHFM_DEV void load(const void* p) {
-    const float4 x = *reinterpret_cast<const float4*>(p);
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+    const u32x4_t x = load16<NT>(p);
+    v[0] = __uint_as_float(x[0]); v[1] = __uint_as_float(x[1]);
+    v[2] = __uint_as_float(x[2]); v[3] = __uint_as_float(x[3]);
   }
 };
 
@@ -30,13 +50,13 @@ template <>
 struct Chunk<true> {
   static constexpr int kElems = 8;
   float v[8];
+  template <bool NT = false>
   HHFM_DEV void load(const void* p) {
-    const uint4 x = *reinterpret_cast<const uint4*>(p);
-    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+    const u32x4_t x = load16<NT>(p);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);             // low bf16
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);  // high bf16
+      v[2 * i] = __uint_as_float(x[i] << 16);             // low bf16
+      v[2 * i + 1] = __uint_as_float(x[i] & 0xffff0000u);  // high bf16
     }
   }
 };

@@ -49,6 +49,19 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_fm_score_rows");
         });
 
+  m.def("fm_score_rows_ex",
+        [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype,
+           uptr w, float w0, uptr out, int flags, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_fm_score_rows_ex(P<const int32_t>(idx), B, F, P<const void>(E),
+                                       M, k, dtype, P<const float>(w), w0,
+                                       P<float>(out), flags, P<void>(stream));
+          }
+          check(rc, "hhfm_fm_score_rows_ex");
+        });
+
   m.def("hybrid_score_rows",
         [](uptr idx, int64_t B, int ncols, int ucol, int icol, int c0, int c1,
            int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr out,

@@ -61,6 +61,17 @@ int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                        int32_t dtype, const float* w, float w0, float* out,
                        void* stream);
 
+/* Same, with tuning flags:
+ *   HHFM_FLAG_STREAM_TABLE — read embedding rows / ids and write `out` with
+ *   non-temporal accesses, so the small, re-read bias table w stays resident
+ *   in L2 / the 256 MB Infinity Cache while the (huge) table streams past. */
+#define HHFM_FLAG_STREAM_TABLE 1
+#define HHFM_FM_ROWS_DEFAULT_FLAGS 0
+int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
+                          const void* E, int64_t features_M, int32_t k,
+                          int32_t dtype, const float* w, float w0, float* out,
+                          int32_t flags, void* stream);
+
 /* ------------------------------------------------------------------------
  * H1 — HHFM per-row score (replaces `OUR.PositiveFeadback`,
  * OurModel7.py:105-171 with sum pooling, :14-19)
