@@ -88,6 +88,13 @@ HHFM_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
+// Order-preserving float <-> int32 key (signed compare == float compare).
+HHFM_DEV int32_t fkey(float f) {
+  const int32_t b = __float_as_int(f);
+  return b >= 0 ? b : (b ^ 0x7fffffff);
+}
+HHFM_DEV float fkey_inv(int32_t k) { return __int_as_float(k >= 0 ? k : (k ^ 0x7fffffff)); }
+
 template <int KPAD>
 HHFM_DEV void insert_one(float* ls, int32_t* li, float s, int32_t it, int K) {
   const int l = lane_id();
@@ -112,7 +119,7 @@ __global__ __launch_bounds__(256) void catalog_main(
     const char* __restrict__ E, int64_t item_row_begin, int32_t N,
     const float* __restrict__ w, int K, int S, int tiles_per_split, int nqb,
     float* __restrict__ out_s, int32_t* __restrict__ out_i, int64_t ostride_b,
-    int64_t ostride_s, int32_t gbase) {
+    int64_t ostride_s, int32_t gbase, int32_t* __restrict__ gthr) {
   constexpr int k = BF16 ? KT * 16 : KT * 8;   // factors
   constexpr int64_t ROWB = (int64_t)KT * 32;   // bytes per embedding row
   constexpr int EPC = BF16 ? 8 : 4;            // k-elements per 16-B chunk
@@ -215,6 +222,10 @@ __global__ __launch_bounds__(256) void catalog_main(
     }
 
     // ---- filter against the per-query K-th score ----
+    // The threshold is the better of this split's K-th score and the best
+    // K-th score any split has published for the query (gthr: monotone
+    // atomicMax hint; a stale value only admits extra candidates).
+    if (q < B) thr = fmaxf(thr, fkey_inv(gthr[q]));
     const int ibase = tile * kTile;
     bool pass[16];
     int count = 0;
@@ -274,7 +285,13 @@ __global__ __launch_bounds__(256) void catalog_main(
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    if (q < B) thr = ls[j * KPAD + (K - 1)];
+    if (q < B) {
+      const float kth = ls[j * KPAD + (K - 1)];
+      if (kth > thr) {
+        thr = kth;
+        if (h == 0) atomicMax(gthr + q, fkey(kth));   // publish for other splits
+      }
+    }
   }
 
   // ---- emit this split's sorted list per query ----
@@ -324,7 +341,7 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 struct Plan {
   int64_t Bpad;
   int nqb, S, tiles_per_split;
-  size_t off_H, off_cst, off_ps, off_pi, total;
+  size_t off_H, off_cst, off_thr, off_ps, off_pi, total;
 };
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -346,6 +363,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   size_t off = 0;
   p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
   p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
+  p.off_thr = off; off += align256((size_t)p.Bpad * sizeof(int32_t));
   p.off_ps = off;
   if (p.S > 1) {
     off += align256((size_t)B * p.S * K * sizeof(float));
@@ -362,23 +380,24 @@ template <bool BF16, int KT, int KPAD, bool FM>
 static void launch_main(const Plan& p, const float* H, const float* cst, int64_t B,
                         const char* E, int64_t item_row_begin, int32_t N,
                         const float* w, int K, float* os, int32_t* oi,
-                        int64_t sb, int64_t ss, int32_t gbase, hipStream_t st) {
+                        int64_t sb, int64_t ss, int32_t gbase, int32_t* gthr,
+                        hipStream_t st) {
   hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM>), dim3(p.nqb * p.S),
                      dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
-                     p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase);
+                     p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
 }
 
 template <bool BF16, int KPAD, bool FM>
 static bool dispatch_kt(int KT, const Plan& p, const float* H, const float* cst,
                         int64_t B, const char* E, int64_t irb, int32_t N,
                         const float* w, int K, float* os, int32_t* oi, int64_t sb,
-                        int64_t ss, int32_t gbase, hipStream_t st) {
+                        int64_t ss, int32_t gbase, int32_t* gthr, hipStream_t st) {
   switch (KT) {
-    case 1: launch_main<BF16, 1, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
-    case 2: launch_main<BF16, 2, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
-    case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
-    case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
-    case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, st); break;
+    case 1: launch_main<BF16, 1, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 2: launch_main<BF16, 2, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
     default: return false;
   }
   return true;
@@ -444,7 +463,10 @@ extern "C" int hhfm_catalog_topk(
   char* ws = reinterpret_cast<char*>(workspace);
   float* H = reinterpret_cast<float*>(ws + p.off_H);
   float* cst = reinterpret_cast<float*>(ws + p.off_cst);
+  int32_t* gthr = reinterpret_cast<int32_t*>(ws + p.off_thr);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // 0x80808080 decodes to ~-3.4e38: below every finite score
+  hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
   const char* Eb = reinterpret_cast<const char*>(E);
 
   {
@@ -477,7 +499,7 @@ extern "C" int hhfm_catalog_topk(
   const int32_t gbase = global_item_base;  // order-preserving shift
   const bool fm = mode == HHFM_MODE_FM;
   bool ok;
-#define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, st
+#define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, st
   if (K <= 32) {
     if (bf16) ok = fm ? dispatch_kt<true, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<true, 32, false>(HHFM_MAIN_ARGS);
     else ok = fm ? dispatch_kt<false, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<false, 32, false>(HHFM_MAIN_ARGS);

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmarks (one process, HIP events, medians):
+  K1 fm_score_rows  : bench workload with / without w, fp32 / bf16 table
+  H1 hybrid rows    : same shape, HHFM layout
+  K2 catalog_topk   : C3 (HHFM k=64 bf16, Frappe catalog, B=3000 = the 10
+                      evaluate_TopK batches) and a C4 shard (k=128, 1.25 M
+                      items, B=1024, K=20), fp32 and bf16
+Prints one JSON object."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+from hhfm_amd import ops  # noqa: E402
+from hhfm_amd._native import native  # noqa: E402
+
+dev = torch.device("cuda", 0)
+nat = native()
+st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+only = os.environ.get("MB_ONLY", "")
+
+
+def timeit(fn, reps=10, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts)), float(np.min(ts))
+
+
+res = {}
+if not only or "k1" in only:
+    rows = 1 << 25
+    idx, E, w, M = bench.make_batch(rows, 8 << 20, 8 << 20, 64, 1, dev)
+    out = torch.empty(rows, dtype=torch.float32, device=dev)
+    res["k1_f32_w"] = timeit(lambda: ops.fm_score_rows(idx, E, w, 0.0, out=out))
+    res["k1_f32_now"] = timeit(lambda: ops.fm_score_rows(idx, E, None, 0.0, out=out))
+    res["h1_f32"] = timeit(lambda: ops.hybrid_score_rows(idx, E, 0, 1, (2, 5), (0, 0), out=out))
+    Eb = E.to(torch.bfloat16)
+    del E
+    res["k1_bf16_w"] = timeit(lambda: ops.fm_score_rows(idx, Eb, w, 0.0, out=out))
+    res["h1_bf16"] = timeit(lambda: ops.hybrid_score_rows(idx, Eb, 0, 1, (2, 5), (0, 0), out=out))
+    del Eb, idx, w, out
+    torch.cuda.empty_cache()
+
+if not only or "k2" in only:
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    for name, nu, ni, k, B, dt in [("c3_hhfm_k64_bf16", 957, 4082, 64, 3000, torch.bfloat16),
+                                   ("c3_hhfm_k64_f32", 957, 4082, 64, 3000, torch.float32),
+                                   ("c4_shard_k128_f32", 1 << 20, 1_250_000, 128, 1024, torch.float32),
+                                   ("c4_shard_k128_bf16", 1 << 20, 1_250_000, 128, 1024, torch.bfloat16)]:
+        M = nu + ni + 12
+        E = (torch.randn(M, k, generator=g, device=dev) * 0.01).to(dt)
+        cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
+                torch.randint(nu, nu + ni, (B,), generator=g, device=dev)]
+        off = nu + ni
+        for c in (7, 2, 3):
+            cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+            off += c
+        A = torch.stack(cols, 1).to(torch.int32).contiguous()
+        fn = lambda: ops.catalog_topk(A, E, ops.MODE_HHFM, 20, nu, ni, 0, None, 0, (2, 5), (0, 0))  # noqa
+        med, mn = timeit(fn, reps=10)
+        flops = 2.0 * B * ni * k
+        res[name] = {"median_ms": med, "min_ms": mn, "TFLOPs": flops / (med * 1e-3) / 1e12,
+                     "pairs_per_s": B * ni / (med * 1e-3)}
+        del E
+        torch.cuda.empty_cache()
+print(json.dumps(res, indent=1))
