@@ -184,6 +184,8 @@ __global__ __launch_bounds__(256) void catalog_main(
   if (tb0 < tb1) load_tile(tb0);
 
   for (int tile = tb0; tile < tb1; ++tile) {
+    // global threshold hint: load now, consume after the MFMA chain
+    const int32_t gk = (q < B) ? gthr[q] : 0;
     f32x16 acc = {0};
     const int nxt = tile + 1 < tb1 ? tile + 1 : tile;
     float wcur = wi;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void catalog_main(
     // The threshold is the better of this split's K-th score and the best
     // K-th score any split has published for the query (gthr: monotone
     // atomicMax hint; a stale value only admits extra candidates).
-    if (q < B) thr = fmaxf(thr, fkey_inv(gthr[q]));
+    if (q < B) thr = fmaxf(thr, fkey_inv(gk));
     const int ibase = tile * kTile;
     bool pass[16];
     int count = 0;

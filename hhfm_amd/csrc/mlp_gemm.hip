@@ -1,0 +1,576 @@
+// K3 — DeepFM on gfx950: LDS-tiled MFMA GEMM with a row-gathered A operand
+// and fused epilogues, plus the small kernels around it.
+//
+//   hhfm_dfm_forward        replaces DeepFM.out   (Newcode/DFM.py:104-137)
+//   hhfm_dfm_catalog_topk   replaces DeepFM.topk  (Newcode/DFM.py:219-231)
+//   hhfm_topk_dense         replaces tf.nn.top_k on a materialised [B,N]
+//                           score matrix (DFM.py:230, AFM.py:245)
+//
+// GEMM tile: 128 x 128 per 256-thread workgroup (4 waves, 2x2, 64x64 per
+// wave); K staged through double-buffered LDS with one barrier per K-step.
+//   bf16 mode: v_mfma_f32_16x16x32_bf16, BK = 32, fp32 accumulate;
+//   f32  mode: v_mfma_f32_16x16x4_f32  (exact fp32 fmaf chains), BK = 16,
+//              each lane reads 4 consecutive k with one ds_read_b128 and
+//              feeds them to 4 MFMAs (k-permuted identically for A and B).
+// A modes: dense [M][lda] (hidden activations) or gathered — row m is the
+// concatenation of the F field embeddings E[idx[m][f]] (DFM.py:104,125), read
+// straight from the table (no [B, F*k] staging buffer in HBM).
+// Epilogues: (a) relu(acc + bias) stored as bf16 / f32 (DFM.py:127-128);
+// (b) relu(acc + bias) · v summed over the tile's columns into per-row
+// partials (last hidden layer fused with the concat projection, DFM.py:137).
+#include "topk_common.h"
+
+namespace hhfm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int GBM = 128, GBN = 128;
+
+struct GemmArgs {
+  int64_t M;
+  int N, K;
+  const void* A;       // dense A [M][lda] in compute dtype
+  int64_t lda;
+  const int32_t* gidx;  // gather mode: idx [M][F]; A[m] = concat_f T[idx[m][f]]
+  const void* T;        // table [Mtab][kf]
+  int64_t Mtab;
+  int F, kf, t_bf16;    // table row width / dtype
+  const void* Bt;       // weights, transposed: [N][ldb] (K contiguous), compute dtype
+  int64_t ldb;
+  const float* bias;    // [N] or null
+  int relu;
+  void* C;              // epilogue store: [M][ldc]
+  int64_t ldc;
+  int c_bf16;
+  const float* dotv;    // epilogue dot: v[N]
+  float* partial;       // [M][gridDim.y]
+};
+
+HHFM_DEV uint16_t f2bf(float f) {  // round to nearest even (finite inputs)
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// One 16-byte LDS chunk of A or B: 8 bf16 (bf16 mode) or 4 f32 (f32 mode).
+template <bool BF>
+struct Stage {
+  static constexpr int kElems = BF ? 8 : 4;
+  u32x4_t v;
+};
+
+// Load the 16-B chunk of A at (row m, k offset kk) in compute dtype.
+template <bool BF>
+HHFM_DEV u32x4_t load_a_chunk(const GemmArgs& g, int64_t m, int kk) {
+  u32x4_t z = {0, 0, 0, 0};
+  if (m >= g.M || kk >= g.K) return z;
+  if (!g.gidx) {
+    const char* p = reinterpret_cast<const char*>(g.A) + (m * g.lda + kk) * (BF ? 2 : 4);
+    return *reinterpret_cast<const u32x4_t*>(p);
+  }
+  const int f = kk / g.kf, c = kk - f * g.kf;
+  const int32_t id = clamp_id(g.gidx[m * g.F + f], g.Mtab);
+  if (g.t_bf16) {
+    const uint16_t* row = reinterpret_cast<const uint16_t*>(g.T) + (int64_t)id * g.kf + c;
+    if (BF) return *reinterpret_cast<const u32x4_t*>(row);   // 8 bf16
+    const uint2 x = *reinterpret_cast<const uint2*>(row);      // 4 bf16 -> 4 f32
+    u32x4_t r = {x.x << 16, x.x & 0xffff0000u, x.y << 16, x.y & 0xffff0000u};
+    return r;
+  }
+  const float* row = reinterpret_cast<const float*>(g.T) + (int64_t)id * g.kf + c;
+  if (!BF) return *reinterpret_cast<const u32x4_t*>(row);      // 4 f32
+  const float4 a = *reinterpret_cast<const float4*>(row);      // 8 f32 -> 8 bf16
+  const float4 b = *reinterpret_cast<const float4*>(row + 4);
+  u32x4_t r = {(uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16),
+               (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16),
+               (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16),
+               (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16)};
+  return r;
+}
+
+template <bool BF>
+HHFM_DEV u32x4_t load_b_chunk(const GemmArgs& g, int n, int kk) {
+  u32x4_t z = {0, 0, 0, 0};
+  if (n >= g.N || kk >= g.K) return z;
+  const char* p = reinterpret_cast<const char*>(g.Bt) + ((int64_t)n * g.ldb + kk) * (BF ? 2 : 4);
+  return *reinterpret_cast<const u32x4_t*>(p);
+}
+
+template <bool BF, int EPI>
+__global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
+  constexpr int EL = BF ? 8 : 4;          // elements per 16-B chunk
+  constexpr int BK = BF ? 32 : 16;        // K per stage (= 4 chunks per row)
+  constexpr int CPR = BK / EL;            // chunks per tile row (4)
+  constexpr int LDR = CPR + 1;            // LDS row stride in chunks (+1 pad)
+  __shared__ u32x4_t As[2][GBM * LDR];
+  __shared__ u32x4_t Bs[2][GBN * LDR];
+  __shared__ float red[2][GBM];
+
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int wm = wv >> 1, wn = wv & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * GBM;
+  const int n0 = blockIdx.y * GBN;
+  const int nk = (g.K + BK - 1) / BK;
+
+  // each thread stages 2 A chunks and 2 B chunks per K-step
+  u32x4_t ra[2], rb[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, r = c / CPR, p = c % CPR;
+      ra[i] = load_a_chunk<BF>(g, m0 + r, kt * BK + p * EL);
+      rb[i] = load_b_chunk<BF>(g, n0 + r, kt * BK + p * EL);
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, r = c / CPR, p = c % CPR;
+      As[buf][r * LDR + p] = ra[i];
+      Bs[buf][r * LDR + p] = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload(kt + 1);
+    const int ar = wm * 64 + (l & 15), br = wn * 64 + (l & 15), ch = l >> 4;
+    if constexpr (BF) {
+      // 16x16x32: lane holds A[row][8*ch .. +8], B[8*ch .. +8][col]
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const u32x4_t x = As[buf][(ar + 16 * a) * LDR + ch];
+        fa[a] = __builtin_bit_cast(bf16x8, x);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const u32x4_t x = Bs[buf][(br + 16 * b) * LDR + ch];
+        fb[b] = __builtin_bit_cast(bf16x8, x);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    } else {
+      // 16x16x4 f32: lane reads k = 4*ch .. +4 and feeds MFMA j with k = 4*ch + j
+      u32x4_t fa[4], fb[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) fa[a] = As[buf][(ar + 16 * a) * LDR + ch];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) fb[b] = Bs[buf][(br + 16 * b) * LDR + ch];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                __uint_as_float(fa[a][j]), __uint_as_float(fb[b][j]), acc[a][b], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: C/D layout col = l&15, row = 4*(l>>4) + r ----
+  const int col_l = l & 15, rq = (l >> 4) * 4;
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 64 + 16 * b + col_l;
+      const float bn = (g.bias && n < g.N) ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wm * 64 + 16 * a + rq + r;
+          if (m < g.M && n < g.ldc) {
+            float v = acc[a][b][r] + bn;
+            if (g.relu) v = fmaxf(v, 0.f);
+            if (n >= g.N) v = 0.f;  // zero pad columns: next layer's K padding
+            if (g.c_bf16)
+              reinterpret_cast<uint16_t*>(g.C)[m * g.ldc + n] = f2bf(v);
+            else
+              reinterpret_cast<float*>(g.C)[m * g.ldc + n] = v;
+          }
+        }
+    }
+  } else {
+    float part[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[a][r] = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int n = n0 + wn * 64 + 16 * b + col_l;
+      const bool ok = n < g.N;
+      const float bn = (ok && g.bias) ? g.bias[n] : 0.f;
+      const float vn = ok ? g.dotv[n] : 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[a][b][r] + bn;
+          if (g.relu) v = fmaxf(v, 0.f);
+          part[a][r] += ok ? v * vn : 0.f;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = group_sum<16>(part[a][r]);
+        if (col_l == 0) red[wn][wm * 64 + 16 * a + rq + r] = s;
+      }
+    __syncthreads();
+    if (tid < GBM) {
+      const int64_t m = m0 + tid;
+      if (m < g.M) g.partial[m * gridDim.y + blockIdx.y] = red[0][tid] + red[1][tid];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FM part of DeepFM and the final reduce
+//   base[m] = Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c] + bp        (DFM.py:109-122,132,137)
+//   out[m]  = base[m] + Σ_t partial[m][t]
+// ---------------------------------------------------------------------------
+template <bool TBF>
+__global__ __launch_bounds__(256) void dfm_fm_part(const int32_t* __restrict__ idx,
+                                                   int64_t B, int F, const void* __restrict__ E,
+                                                   int64_t M, int k, const float* __restrict__ w,
+                                                   const float* __restrict__ Wp, float bp,
+                                                   float* __restrict__ base) {
+  const int l = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* p = idx + m * F;
+    float acc = 0.f;
+    for (int c = l; c < k; c += kWave) {
+      float s = 0.f, q = 0.f;
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = clamp_id(p[f], M);
+        const float v = TBF ? bf16_to_f32(reinterpret_cast<const uint16_t*>(E)[id * k + c])
+                            : reinterpret_cast<const float*>(E)[id * k + c];
+        s += v;
+        q += v * v;
+      }
+      acc += 0.5f * (s * s - q) * Wp[F + c];
+    }
+    acc = group_sum<kWave>(acc);
+    if (l == 0) {
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) y1 += w[clamp_id(p[f], M)] * Wp[f];
+      base[m] = (y1 + acc) + bp;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void dfm_reduce(const float* __restrict__ base,
+                                                  const float* __restrict__ partial, int nt,
+                                                  int64_t B, float* __restrict__ out) {
+  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= B) return;
+  float s = 0.f;
+  for (int t = 0; t < nt; ++t) s += partial[m * nt + t];
+  out[m] = base[m] + s;
+}
+
+// rows[b*N + i] = qidx[b] with column item_col replaced by item_row_begin + i
+__global__ __launch_bounds__(256) void dfm_build_rows(const int32_t* __restrict__ q, int64_t B,
+                                                      int F, int item_col, int32_t item_row_begin,
+                                                      int32_t N, int32_t* __restrict__ rows) {
+  const int64_t total = B * (int64_t)N * F;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int f = (int)(x % F);
+    const int64_t r = x / F;
+    const int64_t b = r / N;
+    const int32_t i = (int32_t)(r - b * N);
+    rows[x] = f == item_col ? item_row_begin + i : q[b * F + f];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// dense top-K over materialised scores [B][N] (wave per query)
+// ---------------------------------------------------------------------------
+template <int KPAD>
+__global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict__ S,
+                                                         int64_t B, int32_t N, int64_t lds,
+                                                         int K, int32_t base,
+                                                         float* __restrict__ out_s,
+                                                         int32_t* __restrict__ out_i) {
+  const int l = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t b = wave; b < B; b += nwave) {
+    const float* row = S + b * lds;
+    float ls = kNegInf;
+    int32_t li = kNoIdx;
+    float thr = kNegInf;
+    for (int32_t c0 = 0; c0 < N; c0 += kWave) {
+      const int32_t i = c0 + l;
+      const float s = i < N ? row[i] : kNegInf;
+      const bool pass = i < N && s >= thr;
+      const uint64_t m = __ballot(pass);
+      const int cnt = __popcll(m);
+      if (cnt == 0) continue;
+      if (cnt > 8) {
+        float cs = pass ? s : kNegInf;
+        int32_t ci = pass ? i : kNoIdx;
+        bitonic_sort_desc<64>(cs, ci);
+        merge_lists<KPAD>(ls, li, cs, ci);
+      } else {
+        uint64_t mm = m;
+        while (mm) {
+          const int L = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L));
+          const int32_t ic = c0 + L;
+          const int pos = __popcll(__ballot(l < KPAD && better(ls, li, sc, ic)));
+          if (pos < K) {
+            const float ps = __shfl_up(ls, 1, kWave);
+            const int32_t pi = __shfl_up(li, 1, kWave);
+            if (l > pos) { ls = ps; li = pi; }
+            else if (l == pos) { ls = sc; li = ic; }
+          }
+        }
+      }
+      if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
+      thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1));
+    }
+    if (l < K) {
+      out_s[b * K + l] = ls;
+      out_i[b * K + l] = li == kNoIdx ? kNoIdx : li + base;
+    }
+  }
+}
+
+static void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds, int K,
+                              int32_t base, float* os, int32_t* oi, hipStream_t st) {
+  int64_t blocks = (B + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  if (K <= 32)
+    hipLaunchKernelGGL(topk_dense_kernel<32>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+                       K, base, os, oi);
+  else
+    hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+                       K, base, os, oi);
+}
+
+static void launch_gemm(const GemmArgs& g, bool bf, int epi, hipStream_t st) {
+  dim3 grid((unsigned)((g.M + GBM - 1) / GBM), (unsigned)((g.N + GBN - 1) / GBN));
+  if (bf) {
+    if (epi) hipLaunchKernelGGL((gemm_mfma<true, 1>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_mfma<true, 0>), grid, dim3(256), 0, st, g);
+  } else {
+    if (epi) hipLaunchKernelGGL((gemm_mfma<false, 1>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((gemm_mfma<false, 0>), grid, dim3(256), 0, st, g);
+  }
+}
+
+// workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL]
+struct DfmPlan {
+  size_t off_base, off_part, off_h0, off_h1, total;
+  int maxL, ntl;
+};
+
+static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+// activations / weights keep their K dimension padded to 8 (16-B rows)
+static int pad8(int x) { return (x + 7) & ~7; }
+
+static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype) {
+  DfmPlan p{};
+  p.maxL = 0;
+  for (int i = 0; i < nlayers; ++i) p.maxL = pad8(dims[i]) > p.maxL ? pad8(dims[i]) : p.maxL;
+  p.ntl = (dims[nlayers - 1] + GBN - 1) / GBN;
+  const size_t esz = mlp_dtype == HHFM_BF16 ? 2 : 4;
+  size_t off = 0;
+  p.off_base = off; off += al256((size_t)B * 4);
+  p.off_part = off; off += al256((size_t)B * p.ntl * 4);
+  p.off_h0 = off; off += al256((size_t)B * p.maxL * esz);
+  p.off_h1 = off; off += al256((size_t)B * p.maxL * esz);
+  p.total = off;
+  return p;
+}
+
+static int dfm_check(int64_t B, int32_t F, int32_t k, int32_t dtype, int32_t nlayers,
+                     const int32_t* dims, int32_t mlp_dtype) {
+  if (B < 0 || F < 1 || k < 1 || nlayers < 1 || nlayers > 16 || !dims) return HHFM_EINVAL;
+  if ((dtype != HHFM_F32 && dtype != HHFM_BF16) ||
+      (mlp_dtype != HHFM_F32 && mlp_dtype != HHFM_BF16))
+    return HHFM_EINVAL;
+  const int el = mlp_dtype == HHFM_BF16 ? 8 : 4;
+  if (k % el) return HHFM_EUNSUPPORTED;  // gathered A chunks never straddle fields
+  for (int i = 0; i < nlayers; ++i)
+    if (dims[i] < 1) return HHFM_EINVAL;
+  return HHFM_OK;
+}
+
+static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                            int64_t M, int32_t k, int32_t dtype, const float* w,
+                            int32_t nlayers, const int32_t* dims, const void* const* Wt,
+                            const float* const* bias, int32_t mlp_dtype, const float* Wp,
+                            float bp, float* out, char* ws, const DfmPlan& p, hipStream_t st) {
+  const bool bf = mlp_dtype == HHFM_BF16;
+  float* base = reinterpret_cast<float*>(ws + p.off_base);
+  float* part = reinterpret_cast<float*>(ws + p.off_part);
+  void* h[2] = {ws + p.off_h0, ws + p.off_h1};
+  {
+    int64_t blocks = (B + 3) / 4;
+    if (blocks > 8192) blocks = 8192;
+    if (dtype == HHFM_BF16)
+      hipLaunchKernelGGL(dfm_fm_part<true>, dim3((int)blocks), dim3(256), 0, st, idx, B, F, E, M,
+                         k, w, Wp, bp, base);
+    else
+      hipLaunchKernelGGL(dfm_fm_part<false>, dim3((int)blocks), dim3(256), 0, st, idx, B, F, E,
+                         M, k, w, Wp, bp, base);
+  }
+  int Kin = F * k;  // layer 0: gathered rows, K = F*k (k % 8 checked)
+  for (int i = 0; i < nlayers; ++i) {
+    GemmArgs g{};
+    g.M = B;
+    g.N = dims[i];
+    g.K = Kin;
+    if (i == 0) {
+      g.gidx = idx; g.T = E; g.Mtab = M; g.F = F; g.kf = k; g.t_bf16 = dtype == HHFM_BF16;
+    } else {
+      g.A = h[(i - 1) & 1]; g.lda = Kin;
+    }
+    g.Bt = Wt[i];
+    g.ldb = Kin;
+    g.bias = bias[i];
+    g.relu = 1;  // DFM.py:128 applies the activation after EVERY layer
+    const bool last = i == nlayers - 1;
+    if (!last) {
+      g.C = h[i & 1]; g.ldc = pad8(dims[i]); g.c_bf16 = bf;
+    } else {
+      g.dotv = Wp + F + k; g.partial = part;
+    }
+    launch_gemm(g, bf, last ? 1 : 0, st);
+    Kin = pad8(dims[i]);
+  }
+  hipLaunchKernelGGL(dfm_reduce, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st, base, part,
+                     p.ntl, B, out);
+  return (int)hipGetLastError();
+}
+
+}  // namespace hhfm
+
+using namespace hhfm;
+
+extern "C" int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_dims,
+                                          int32_t mlp_dtype, size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || nlayers < 1 || !layer_dims) return HHFM_EINVAL;
+  *ws_bytes = dfm_plan(B, nlayers, layer_dims, mlp_dtype).total;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                                int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                                int32_t nlayers, const int32_t* layer_dims,
+                                const void* const* Wt, const float* const* bias,
+                                int32_t mlp_dtype, const float* Wp, float bp, float* out,
+                                void* workspace, size_t ws_bytes, void* stream) {
+  int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
+  if (rc) return rc;
+  if (features_M < 1) return HHFM_EINVAL;
+  if (B == 0) return HHFM_OK;
+  if (!idx || !E || !w || !Wt || !bias || !Wp || !out) return HHFM_EINVAL;
+  for (int i = 0; i < nlayers; ++i)
+    if (!Wt[i] || !bias[i]) return HHFM_EINVAL;
+  const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype);
+  if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
+  return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
+                          mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+// D2: chunk_rows bounds the rows (queries x items) scored per forward pass.
+static int64_t dfm_cat_qchunk(int64_t B, int32_t N, int64_t chunk_rows) {
+  int64_t qc = chunk_rows / N;
+  if (qc < 1) qc = 1;
+  if (qc > B) qc = B;
+  return qc;
+}
+
+extern "C" int hhfm_dfm_catalog_topk_workspace(int64_t B, int32_t F, int32_t item_count,
+                                               int32_t nlayers, const int32_t* layer_dims,
+                                               int32_t mlp_dtype, int64_t chunk_rows,
+                                               size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 1 || item_count < 1 || chunk_rows < 1) return HHFM_EINVAL;
+  const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
+  const int64_t rows = qc * item_count;
+  const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
+  *ws_bytes = p.total + al256((size_t)rows * F * 4) + al256((size_t)rows * 4);
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
+                                     const void* E, int64_t features_M, int32_t k, int32_t dtype,
+                                     const float* w, int32_t nlayers, const int32_t* layer_dims,
+                                     const void* const* Wt, const float* const* bias,
+                                     int32_t mlp_dtype, const float* Wp, float bp,
+                                     int32_t item_row_begin, int32_t item_count,
+                                     int32_t global_item_base, int32_t K, int64_t chunk_rows,
+                                     float* top_score, int32_t* top_idx, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
+  if (rc) return rc;
+  if (item_col < 0 || item_col >= F || item_count < 1 || item_row_begin < 0 ||
+      (int64_t)item_row_begin + item_count > features_M || chunk_rows < 1)
+    return HHFM_EINVAL;
+  if (K < 1 || K > item_count) return HHFM_EINVAL;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!qidx || !E || !w || !Wt || !bias || !Wp || !top_score || !top_idx) return HHFM_EINVAL;
+  const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
+  const int64_t rows = qc * item_count;
+  const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
+  const size_t need = p.total + al256((size_t)rows * F * 4) + al256((size_t)rows * 4);
+  if (!workspace || ws_bytes < need) return HHFM_EWORKSPACE;
+  char* ws = reinterpret_cast<char*>(workspace);
+  int32_t* rbuf = reinterpret_cast<int32_t*>(ws + p.total);
+  float* sc = reinterpret_cast<float*>(ws + p.total + al256((size_t)rows * F * 4));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int64_t b0 = 0; b0 < B; b0 += qc) {
+    const int64_t nb = (B - b0) < qc ? (B - b0) : qc;
+    const int64_t nrows = nb * item_count;
+    int64_t blocks = (nrows * F + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(dfm_build_rows, dim3((unsigned)blocks), dim3(256), 0, st, qidx + b0 * F,
+                       nb, F, item_col, item_row_begin, item_count, rbuf);
+    rc = dfm_forward_impl(rbuf, nrows, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
+                          bias, mlp_dtype, Wp, bp, sc, ws, p, st);
+    if (rc) return rc;
+    launch_topk_dense(sc, nb, item_count, item_count, K, global_item_base, top_score + b0 * K,
+                      top_idx + b0 * K, st);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,
+                               int32_t global_item_base, float* top_score, int32_t* top_idx,
+                               void* stream) {
+  if (B < 0 || N < 1 || ld < N || K < 1 || K > N) return HHFM_EINVAL;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!scores || !top_score || !top_idx) return HHFM_EINVAL;
+  launch_topk_dense(scores, B, N, ld, K, global_item_base, top_score, top_idx,
+                    reinterpret_cast<hipStream_t>(stream));
+  return (int)hipGetLastError();
+}

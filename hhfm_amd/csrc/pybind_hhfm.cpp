@@ -4,10 +4,12 @@
 // releases the GIL around every launch and turns a non-zero status into an
 // exception.  No torch types cross this boundary.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "hhfm.h"
 
@@ -115,6 +117,88 @@ PYBIND11_MODULE(_hhfm, m) {
                                  P<void>(stream));
           }
           check(rc, "hhfm_topk_merge");
+        });
+
+  m.def("dfm_forward_workspace",
+        [](int64_t B, std::vector<int32_t> dims, int mlp_dtype) {
+          size_t ws = 0;
+          check(hhfm_dfm_forward_workspace(B, (int)dims.size(), dims.data(), mlp_dtype, &ws),
+                "hhfm_dfm_forward_workspace");
+          return ws;
+        });
+
+  m.def("dfm_forward",
+        [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w,
+           std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
+           int mlp_dtype, uptr Wp, float bp, uptr out, uptr ws, size_t ws_bytes,
+           uptr stream) {
+          if (Wt.size() != dims.size() || bias.size() != dims.size())
+            throw py::value_error("dims, Wt and bias must have the same length");
+          std::vector<const void*> W(Wt.size());
+          std::vector<const float*> b(bias.size());
+          for (size_t i = 0; i < W.size(); ++i) {
+            W[i] = P<const void>(Wt[i]);
+            b[i] = P<const float>(bias[i]);
+          }
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_dfm_forward(P<const int32_t>(idx), B, F, P<const void>(E), M, k, dtype,
+                                  P<const float>(w), (int)dims.size(), dims.data(), W.data(),
+                                  b.data(), mlp_dtype, P<const float>(Wp), bp, P<float>(out),
+                                  P<void>(ws), ws_bytes, P<void>(stream));
+          }
+          check(rc, "hhfm_dfm_forward");
+        });
+
+  m.def("dfm_catalog_topk_workspace",
+        [](int64_t B, int F, int item_count, std::vector<int32_t> dims, int mlp_dtype,
+           int64_t chunk_rows) {
+          size_t ws = 0;
+          check(hhfm_dfm_catalog_topk_workspace(B, F, item_count, (int)dims.size(), dims.data(),
+                                                mlp_dtype, chunk_rows, &ws),
+                "hhfm_dfm_catalog_topk_workspace");
+          return ws;
+        });
+
+  m.def("dfm_catalog_topk",
+        [](uptr qidx, int64_t B, int F, int item_col, uptr E, int64_t M, int k, int dtype,
+           uptr w, std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
+           int mlp_dtype, uptr Wp, float bp, int item_row_begin, int item_count,
+           int global_item_base, int K, int64_t chunk_rows, uptr top_score, uptr top_idx,
+           uptr ws, size_t ws_bytes, uptr stream) {
+          if (Wt.size() != dims.size() || bias.size() != dims.size())
+            throw py::value_error("dims, Wt and bias must have the same length");
+          std::vector<const void*> W(Wt.size());
+          std::vector<const float*> b(bias.size());
+          for (size_t i = 0; i < W.size(); ++i) {
+            W[i] = P<const void>(Wt[i]);
+            b[i] = P<const float>(bias[i]);
+          }
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_dfm_catalog_topk(P<const int32_t>(qidx), B, F, item_col, P<const void>(E),
+                                       M, k, dtype, P<const float>(w), (int)dims.size(),
+                                       dims.data(), W.data(), b.data(), mlp_dtype,
+                                       P<const float>(Wp), bp, item_row_begin, item_count,
+                                       global_item_base, K, chunk_rows, P<float>(top_score),
+                                       P<int32_t>(top_idx), P<void>(ws), ws_bytes,
+                                       P<void>(stream));
+          }
+          check(rc, "hhfm_dfm_catalog_topk");
+        });
+
+  m.def("topk_dense",
+        [](uptr scores, int64_t B, int N, int64_t ld, int K, int base, uptr top_score,
+           uptr top_idx, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_topk_dense(P<const float>(scores), B, N, ld, K, base, P<float>(top_score),
+                                 P<int32_t>(top_idx), P<void>(stream));
+          }
+          check(rc, "hhfm_topk_dense");
         });
 
   m.def("topk_merge_host",

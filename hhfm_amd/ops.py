@@ -154,3 +154,86 @@ def topk_merge(scores: torch.Tensor, ids: torch.Tensor
         nat.topk_merge_host(scores.data_ptr(), ids.data_ptr(), R, B, K,
                             out_s.data_ptr(), out_i.data_ptr())
     return out_s, out_i
+
+
+# ---------------------------------------------------------------------------
+# DeepFM (K3) and dense top-K
+# ---------------------------------------------------------------------------
+def _pad8(x: int) -> int:
+    return (x + 7) & ~7
+
+
+def dfm_prepare_weights(layers, biases, mlp_dtype: torch.dtype, F: int, k: int):
+    """Transpose (and pad K to a multiple of 8) the MLP weights into the
+    [N][K] layout the GEMM kernel streams (include/hhfm.h, D1)."""
+    Wt, bs, dims = [], [], []
+    Kin = F * k
+    for W, b in zip(layers, biases):
+        W = torch.as_tensor(W)
+        Kreal, N = W.shape
+        t = torch.zeros(N, Kin, dtype=torch.float32, device=W.device)
+        t[:, :Kreal] = W.t().float()
+        Wt.append(t.to(mlp_dtype).contiguous())
+        bs.append(torch.as_tensor(b).reshape(-1).float().contiguous())
+        dims.append(N)
+        Kin = _pad8(N)
+    return Wt, bs, dims
+
+
+def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
+                mlp_dtype: torch.dtype, Wp: torch.Tensor, bp: float,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B]."""
+    _idx(idx, "idx")
+    dev = _need_cuda(idx, E, w, Wp, *Wt, *bias)
+    B, F = idx.shape
+    M, k = E.shape
+    md = _dtype_code(Wt[0])
+    if mlp_dtype != Wt[0].dtype:
+        raise TypeError("Wt dtype must equal mlp_dtype")
+    if out is None:
+        out = torch.empty(B, dtype=torch.float32, device=dev)
+    nat = native()
+    ws = _workspace(dev, nat.dfm_forward_workspace(B, list(dims), md))
+    nat.dfm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
+                    list(dims), [t.data_ptr() for t in Wt], [t.data_ptr() for t in bias], md,
+                    Wp.data_ptr(), float(bp), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                    _stream(dev))
+    return out
+
+
+def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
+                     Wp: torch.Tensor, bp: float, item_col: int, item_row_begin: int,
+                     item_count: int, K: int, global_item_base: int = 0,
+                     chunk_rows: int = 1 << 20):
+    """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K])."""
+    _idx(qidx, "qidx")
+    dev = _need_cuda(qidx, E, w, Wp, *Wt, *bias)
+    B, F = qidx.shape
+    M, k = E.shape
+    md = _dtype_code(Wt[0])
+    nat = native()
+    ws = _workspace(dev, nat.dfm_catalog_topk_workspace(B, F, item_count, list(dims), md,
+                                                        chunk_rows))
+    top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
+    top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
+    nat.dfm_catalog_topk(qidx.data_ptr(), B, F, item_col, E.data_ptr(), M, k, _dtype_code(E),
+                         w.data_ptr(), list(dims), [t.data_ptr() for t in Wt],
+                         [t.data_ptr() for t in bias], md, Wp.data_ptr(), float(bp),
+                         item_row_begin, item_count, global_item_base, K, chunk_rows,
+                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), ws.numel(),
+                         _stream(dev))
+    return top_s, top_i
+
+
+def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0):
+    """tf.nn.top_k over a device score matrix [B, N] (K <= 64)."""
+    _need_cuda(scores)
+    if scores.dtype != torch.float32 or scores.dim() != 2:
+        raise TypeError("scores must be float32 [B, N]")
+    B, N = scores.shape
+    top_s = torch.empty(B, K, dtype=torch.float32, device=scores.device)
+    top_i = torch.empty(B, K, dtype=torch.int32, device=scores.device)
+    native().topk_dense(scores.data_ptr(), B, N, scores.stride(0), K, global_item_base,
+                        top_s.data_ptr(), top_i.data_ptr(), _stream(scores.device))
+    return top_s, top_i

@@ -128,6 +128,52 @@ int hhfm_topk_merge_host(const float* in_score, const int32_t* in_idx,
                          int32_t R, int64_t B, int32_t K, float* out_score,
                          int32_t* out_idx);
 
+/* ------------------------------------------------------------------------
+ * D1 — DeepFM per-row score (replaces `DeepFM.out`, DFM.py:104-137)
+ *   y1 = w[x] (F), y2 = ½((Σe)² − Σe²) (k), h_0 = concat_f E[x_f] (F·k),
+ *   h_{i+1} = relu(h_i · W_i + b_i) for every layer (ReLU after the last one
+ *   too, DFM.py:128), out = [y1, y2, h_L] · Wp + bp.
+ * Wt[i] are DEVICE pointers to the layer weights TRANSPOSED, [dims[i]][K_i]
+ * with K_0 = F·k and K_i = dims[i-1] rounded up to a multiple of 8 (pad
+ * columns zero), in mlp_dtype; bias[i] device float [dims[i]];
+ * the Wt/bias/layer_dims arrays themselves are host arrays.  mlp_dtype
+ * HHFM_F32 runs exact-fp32 MFMA (v_mfma_f32_16x16x4_f32), HHFM_BF16 runs
+ * bf16 MFMA with fp32 accumulation (activations rounded to bf16).
+ * Wp: device float [F + k + dims[L-1]].  k must be a multiple of 4 (f32) /
+ * 8 (bf16); layer widths are arbitrary.
+ * ---------------------------------------------------------------------- */
+int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_dims,
+                               int32_t mlp_dtype, size_t* ws_bytes);
+int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                     int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                     int32_t nlayers, const int32_t* layer_dims, const void* const* Wt,
+                     const float* const* bias, int32_t mlp_dtype, const float* Wp,
+                     float bp, float* out, void* workspace, size_t ws_bytes,
+                     void* stream);
+
+/* D2 — DeepFM.topk (DFM.py:219-231): every query row is tiled over the
+ * catalog with column item_col replaced by each item id, scored by D1 and
+ * top-K selected; at most chunk_rows (query x item) rows per pass. */
+int hhfm_dfm_catalog_topk_workspace(int64_t B, int32_t F, int32_t item_count,
+                                    int32_t nlayers, const int32_t* layer_dims,
+                                    int32_t mlp_dtype, int64_t chunk_rows,
+                                    size_t* ws_bytes);
+int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
+                          const void* E, int64_t features_M, int32_t k, int32_t dtype,
+                          const float* w, int32_t nlayers, const int32_t* layer_dims,
+                          const void* const* Wt, const float* const* bias,
+                          int32_t mlp_dtype, const float* Wp, float bp,
+                          int32_t item_row_begin, int32_t item_count,
+                          int32_t global_item_base, int32_t K, int64_t chunk_rows,
+                          float* top_score, int32_t* top_idx, void* workspace,
+                          size_t ws_bytes, void* stream);
+
+/* tf.nn.top_k(scores, K) over a materialised score matrix [B][ld] (first N
+ * columns), K <= 64; ids reported as global_item_base + column. */
+int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,
+                    int32_t global_item_base, float* top_score, int32_t* top_idx,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

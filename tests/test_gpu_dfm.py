@@ -1,0 +1,146 @@
+"""DeepFM (K3) on the GPU vs the reference graph (golden dfm.npz) and vs the
+oracle at larger shapes.
+
+Tolerances: fp32 MLP mode (exact-fp32 MFMA, reference numerics) — 2e-5 of
+the output's natural magnitude Σ_j |concat_j·Wp_j| + |bp|; bf16 MLP mode —
+compared with an oracle that rounds the same operands to bf16 (table rows,
+weights, hidden activations), 5e-3 of that magnitude (a 1-ulp bf16 flip of a
+hidden unit, 2^-8 relative, is the expected discrepancy)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fm_oracle as orc
+from tests.helpers import bf16_round
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _model(d_or_shapes, mlp_dtype=torch.float32, table_dtype=torch.float32):
+    from hhfm_amd.DFM import DeepFM
+    nu, ni, M, F, k, layers = d_or_shapes
+    return DeepFM(nu, ni, M, F, k, layers, None, 0.01, 0, 0.01, mlp_dtype=mlp_dtype,
+                  table_dtype=table_dtype)
+
+
+def _magnitude(X, E, w, layers, biases, Wp, bp):
+    """Σ_j |concat_j · Wp_j| + |bp| in float64 (natural scale of the output)."""
+    X = np.asarray(X, np.int64)
+    e = E[X].astype(np.float64)
+    y1 = w[X].astype(np.float64)
+    s = e.sum(1)
+    y2 = 0.5 * (s * s - (e * e).sum(1))
+    h = e.reshape(len(X), -1)
+    for Wl, bl in zip(layers, biases):
+        h = np.maximum(h @ Wl.astype(np.float64) + bl.astype(np.float64), 0)
+    cat = np.concatenate([y1, y2, h], 1)
+    return (np.abs(cat * Wp.reshape(1, -1))).sum(1) + abs(float(bp))
+
+
+def _bf16_oracle(X, E, w, layers, biases, Wp, bp):
+    """bf16 MLP mode: table rows, weights and stored hidden activations rounded
+    to bf16; accumulation and the final dot in fp32; FM part in fp32."""
+    X = np.asarray(X, np.int64)
+    e = E[X]
+    y1 = w[X]
+    s = e.sum(1, dtype=np.float32)
+    y2 = np.float32(0.5) * (s * s - (e * e).sum(1, dtype=np.float32))
+    h = bf16_round(e.reshape(len(X), -1))
+    L = len(layers)
+    for i, (Wl, bl) in enumerate(zip(layers, biases)):
+        h = np.maximum(h @ bf16_round(Wl) + bl, 0).astype(np.float32)
+        if i < L - 1:
+            h = bf16_round(h)
+    cat = np.concatenate([y1, y2, h], 1)
+    return (cat @ Wp.reshape(-1, 1))[:, 0] + np.float32(bp)
+
+
+def test_dfm_vs_reference_graph():
+    d = dict(np.load(os.path.join(G, "dfm.npz")))
+    nu, ni = int(d["n_user"]), int(d["n_item"])
+    M, k = d["E"].shape
+    layers = [d[f"layer_{i}"] for i in range(3)]
+    biases = [d[f"bias_{i}"] for i in range(3)]
+    m = _model((nu, ni, M, 5, k, [150, 200, 150]))
+    m.set_weights(feature_embeddings=d["E"], feature_bias=d["w"][:, None],
+                  concat_projection=d["concat_projection"], concat_bias=d["concat_bias"],
+                  **{f"layer_{i}": layers[i] for i in range(3)},
+                  **{f"bias_{i}": biases[i] for i in range(3)})
+    out = m.score_rows(d["X"])[:, 0]
+    mag = _magnitude(d["X"], d["E"], d["w"], layers, biases, d["concat_projection"], d["concat_bias"])
+    assert np.all(np.abs(out - d["out"]) <= 2e-5 * mag)
+    out2 = m.sess.run(m.out, feed_dict={m.feat_index: d["X"], m.label: None})
+    assert np.array_equal(out2[:, 0], out)
+    pred = m.topk(d["A"], 20)
+    rs, ri = orc.top_k(d["topk_scores"], 21)
+    tol = 2e-5 * np.abs(d["topk_scores"]).max(1, keepdims=True) * 10
+    mism, amb = orc.topk_index_agreement(rs, ri[:, :20], pred, tol)
+    assert mism == 0, (mism, amb)
+
+
+@pytest.mark.parametrize("mlp", ["f32", "bf16"])
+@pytest.mark.parametrize("k,layers", [(64, [400, 400, 400]), (256, [400, 400, 400]),
+                                      (32, [150, 200, 150])])
+def test_dfm_forward_shapes(mlp, k, layers):
+    rng = np.random.default_rng(k + len(layers))
+    nu, ni, F = 957, 4082, 5
+    M = nu + ni + 12
+    B = 3001
+    X = np.stack([rng.integers(0, nu, B), rng.integers(nu, nu + ni, B),
+                  rng.integers(nu + ni, nu + ni + 7, B), rng.integers(nu + ni + 7, nu + ni + 9, B),
+                  rng.integers(nu + ni + 9, M, B)], 1).astype(np.int32)
+    mdt = torch.float32 if mlp == "f32" else torch.bfloat16
+    m = _model((nu, ni, M, F, k, layers), mlp_dtype=mdt)
+    W = m.get_weights()
+    Ls = [W[f"layer_{i}"] for i in range(3)]
+    Bs = [W[f"bias_{i}"] for i in range(3)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    got = m.score_rows(X)[:, 0]
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    if mlp == "f32":
+        ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
+        assert np.all(np.abs(got - ref) <= 2e-5 * mag)
+    else:
+        ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+        assert np.all(np.abs(got - ref) <= 5e-3 * mag)
+
+
+def test_dfm_catalog_topk_chunked():
+    """Query chunking (chunk_rows < B*N) gives the same top-K as one pass."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(8)
+    nu, ni, F, k = 50, 700, 5, 32
+    M = nu + ni + 12
+    m = _model((nu, ni, M, F, k, [64, 48]))
+    A = np.stack([rng.integers(0, nu, 37), rng.integers(nu, nu + ni, 37),
+                  rng.integers(nu + ni, nu + ni + 7, 37), rng.integers(nu + ni + 7, nu + ni + 9, 37),
+                  rng.integers(nu + ni + 9, M, 37)], 1).astype(np.int32)
+    W = m.get_weights()
+    Ls = [W["layer_0"], W["layer_1"]]
+    Bs = [W["bias_0"], W["bias_1"]]
+    sc = orc.dfm_catalog_scores(A, W["feature_embeddings"], W["feature_bias"][:, 0], Ls, Bs,
+                                W["concat_projection"], float(W["concat_bias"]), nu, ni)
+    Wt, bs, dims, Wp, bp = m._prepared()
+    q = torch.from_numpy(A).cuda()
+    for chunk in (1 << 20, 1000, 701):
+        s, i = ops.dfm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,
+                                    dims, Wp, bp, 1, nu, ni, 20, 0, chunk)
+        rs, ri = orc.top_k(sc, 21)
+        mism, amb = orc.topk_index_agreement(rs, ri[:, :20], i.cpu().numpy(),
+                                             1e-5 * np.abs(sc).max(1, keepdims=True))
+        assert mism == 0, (chunk, mism, amb)
+
+
+def test_topk_dense_matches_sort():
+    from hhfm_amd import ops
+    rng = np.random.default_rng(3)
+    S = rng.integers(0, 50, size=(77, 3001)).astype(np.float32)   # heavy ties
+    for K in (1, 20, 33, 64):
+        s, i = ops.topk_dense(torch.from_numpy(S).cuda(), K, 5)
+        rs, ri = orc.top_k(S, K)
+        assert np.array_equal(i.cpu().numpy(), ri + 5)
+        assert np.array_equal(s.cpu().numpy(), rs)
