@@ -29,7 +29,7 @@ all: native oracle
 native: $(LIB) $(PYMOD)
 oracle: $(ORACLE)
 
-build/%.o: $(CSRC)/%.hip $(CSRC)/hhfm_common.h include/hhfm.h
+build/%.o: $(CSRC)/%.hip $(wildcard $(CSRC)/*.h) include/hhfm.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

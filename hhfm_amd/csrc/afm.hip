@@ -1,0 +1,331 @@
+// K4 — AFM (attentional FM) on gfx950, on top of the shared MFMA GEMM.
+//
+//   hhfm_afm_forward       replaces AFM.out  (Newcode/AFM.py:103-142)
+//   hhfm_afm_catalog_topk  replaces AFM.topk (Newcode/AFM.py:209-246)
+//
+// A1 (per row): the attention pre-activations of all F(F-1)/2 pair products
+// are one GEMM [B·P, k] x [k, A] whose A operand is formed on the fly as
+// E[x_i] ⊙ E[x_j] (f32 MFMA, exact fp32) and whose epilogue applies
+// relu(· + b)·p and sums over A -> one logit per pair; afm_rows_finish does
+// the pair softmax, Σ att·(e_i ⊙ e_j), the projection P, Σw and w0.
+// A2 (catalog): the item-side pre-activation (uf_f ⊙ item)·W equals
+// item·(diag(uf_f)·W), so for every (query, field) f it is ONE GEMM
+// items [N, k] x W'' [k, B·u_f·A] (W'' built per query by afm_cat_prep) with a
+// grouped epilogue (relu(·+b)·p summed per A-column group) -> logits [N, B·u_f];
+// afm_cat_finish forms the exp-weighted score of AFM.py:232-243 and
+// hhfm_topk_dense selects.  The reference's raw exp (no max subtraction,
+// AFM.py:223,230) is kept.
+#include "gemm_mfma.h"
+
+namespace hhfm {
+
+static size_t a256(size_t x) { return (x + 255) & ~size_t(255); }
+
+HHFM_DEV float tab(const void* E, int bf16, int64_t id, int k, int c) {
+  return bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(E)[id * k + c])
+              : reinterpret_cast<const float*>(E)[id * k + c];
+}
+
+// ---- A1 finish: wave per row --------------------------------------------------
+__global__ __launch_bounds__(256) void afm_rows_finish(
+    const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int t_bf16,
+    int64_t M, int k, const float* __restrict__ w, float w0, const float* __restrict__ P,
+    const float* __restrict__ logit_part, int ntl, float* __restrict__ out) {
+  const int l = lane_id();
+  const int np = F * (F - 1) / 2;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* x = idx + m * F;
+    // logits of this row's pairs (lane p holds pair p; np <= 64 enforced)
+    float lg = kNegInf;
+    if (l < np) {
+      lg = 0.f;
+      for (int t = 0; t < ntl; ++t) lg += logit_part[((m * np) + l) * ntl + t];
+    }
+    float mx = lg;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, kWave));
+    const float e = l < np ? expf(lg - mx) : 0.f;
+    const float s = group_sum<kWave>(e);
+    const float att = e / s;                      // tf.nn.softmax(axis=1), AFM.py:125
+    float bil = 0.f;
+    for (int c = l; c < k; c += kWave) {
+      float afm = 0.f;
+      for (int p = 0; p < np; ++p) {
+        int i, j;
+        pair_ij(p, F, i, j);
+        const float ap = __shfl(att, p, kWave);
+        afm += ap * (tab(E, t_bf16, clamp_id(x[i], M), k, c) * tab(E, t_bf16, clamp_id(x[j], M), k, c));
+      }
+      bil += afm * P[c];                          // AFM·P (AFM.py:138-139)
+    }
+    bil = group_sum<kWave>(bil);
+    if (l == 0) {
+      float fb = 0.f;
+      for (int f = 0; f < F; ++f) fb += w[clamp_id(x[f], M)];
+      out[m] = (bil + fb) + w0;                   // add_n, AFM.py:142
+    }
+  }
+}
+
+// ---- A2 prep: one 64-thread block per query ------------------------------------
+// uf = [E[q0], E[q2], ..., E[q_{F-1}]] (u_f = F-1 fields, AFM.py:210-212)
+constexpr int kAfmMaxK = 256, kAfmMaxUF = 15;
+
+__global__ __launch_bounds__(64) void afm_cat_prep(
+    const int32_t* __restrict__ q, int64_t B, int F, const void* __restrict__ E, int t_bf16,
+    int64_t M, int k, const float* __restrict__ Wt, const float* __restrict__ ab,
+    const float* __restrict__ ap, int A, const float* __restrict__ P,
+    float* __restrict__ W2, float* __restrict__ D, float* __restrict__ ufdot,
+    float* __restrict__ suma) {
+  __shared__ float uf[kAfmMaxUF][kAfmMaxK];
+  __shared__ float pr[kAfmMaxK];
+  const int l = threadIdx.x;
+  const int uF = F - 1;
+  const int64_t b = blockIdx.x;
+  if (b >= B) return;
+  const int32_t* x = q + b * F;
+  for (int f = 0; f < uF; ++f) {
+    const int col = f == 0 ? 0 : f + 1;
+    const int64_t id = clamp_id(x[col], M);
+    for (int c = l; c < k; c += 64) uf[f][c] = tab(E, t_bf16, id, k, c);
+  }
+  __syncthreads();
+  float uw[kAfmMaxK / 64];
+#pragma unroll
+  for (int r = 0; r < kAfmMaxK / 64; ++r) uw[r] = 0.f;
+  float sa = 0.f;
+  for (int i = 0; i < uF; ++i)
+    for (int j = i + 1; j < uF; ++j) {
+      for (int c = l; c < k; c += 64) pr[c] = uf[i][c] * uf[j][c];
+      __syncthreads();
+      float lg = 0.f;
+      for (int a = l; a < A; a += 64) {
+        float acc = 0.f;
+        for (int c = 0; c < k; ++c) acc += pr[c] * Wt[(int64_t)a * k + c];
+        lg += ap[a] * fmaxf(acc + ab[a], 0.f);
+      }
+      lg = group_sum<kWave>(lg);
+      const float aij = expf(lg);                 // raw exp, AFM.py:223
+      sa += aij;
+#pragma unroll
+      for (int r = 0; r < kAfmMaxK / 64; ++r) {
+        const int c = l + 64 * r;
+        if (c < k) uw[r] += aij * pr[c];           // UFwise, AFM.py:232
+      }
+      __syncthreads();
+    }
+  float ud = 0.f;
+#pragma unroll
+  for (int r = 0; r < kAfmMaxK / 64; ++r) {
+    const int c = l + 64 * r;
+    if (c < k) ud += P[c] * uw[r];
+  }
+  ud = group_sum<kWave>(ud);
+  if (l == 0) {
+    ufdot[b] = ud;
+    suma[b] = sa;
+  }
+  // W''[(b*uF+f)*A + a][c] = uf_f[c] * W[c][a];  D[b*uF+f][c] = P[c]*uf_f[c]
+  for (int f = 0; f < uF; ++f) {
+    for (int a = 0; a < A; ++a) {
+      float* dst = W2 + ((b * uF + f) * (int64_t)A + a) * k;
+      for (int c = l; c < k; c += 64) dst[c] = uf[f][c] * Wt[(int64_t)a * k + c];
+    }
+    for (int c = l; c < k; c += 64) D[(b * uF + f) * (int64_t)k + c] = P[c] * uf[f][c];
+  }
+}
+
+// ---- A2 finish: wave per (query, 64-item block), lane = item -------------------
+__global__ __launch_bounds__(256) void afm_cat_finish(
+    int64_t nq, int uF, int A, int G, const float* __restrict__ part, int64_t ldp,
+    const float* __restrict__ D, const float* __restrict__ ufdot, const float* __restrict__ suma,
+    const void* __restrict__ E, int t_bf16, int k, int64_t item_row_begin, int32_t N,
+    const float* __restrict__ w, float* __restrict__ scores) {
+  const int l = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nblk = (N + kWave - 1) / kWave;
+  if (wave >= nq * nblk) return;
+  const int64_t b = wave / nblk;
+  const int32_t i = (int32_t)((wave - b * nblk) * kWave + l);
+  if (i >= N) return;
+  const int gpa = A / G;
+  const int64_t id = item_row_begin + i;
+  float num = ufdot[b], den = suma[b];
+  float extra_num = 0.f, extra_den = 0.f;
+  for (int f = 0; f < uF; ++f) {
+    float lg = 0.f;
+    for (int t = 0; t < gpa; ++t) lg += part[(int64_t)i * ldp + (b * uF + f) * gpa + t];
+    const float a = expf(lg);                      // raw exp, AFM.py:230
+    const float* d = D + (b * uF + f) * (int64_t)k;
+    float dot = 0.f;
+    for (int c = 0; c < k; ++c) dot += d[c] * tab(E, t_bf16, id, k, c);
+    extra_num += a * dot;
+    extra_den += a;
+  }
+  num += extra_num;
+  den += extra_den;
+  scores[b * N + i] = num / den + w[id];           // score3 + bias, AFM.py:239-243
+}
+
+struct AfmCatPlan {
+  int64_t qc;
+  int G;
+  size_t off_W2, off_D, off_ud, off_sa, off_part, off_sc, total;
+};
+
+static AfmCatPlan afm_cat_plan(int64_t B, int F, int k, int A, int N, int64_t max_cols) {
+  AfmCatPlan p{};
+  const int uF = F - 1;
+  p.G = A < 64 ? A : 64;
+  int64_t qc = max_cols / ((int64_t)uF * A);
+  if (qc < 1) qc = 1;
+  if (qc > B) qc = B;
+  p.qc = qc;
+  const int64_t cols = qc * uF * A;
+  size_t off = 0;
+  p.off_W2 = off; off += a256((size_t)cols * k * 4);
+  p.off_D = off; off += a256((size_t)qc * uF * k * 4);
+  p.off_ud = off; off += a256((size_t)qc * 4);
+  p.off_sa = off; off += a256((size_t)qc * 4);
+  p.off_part = off; off += a256((size_t)N * (cols / p.G) * 4);
+  p.off_sc = off; off += a256((size_t)qc * N * 4);
+  p.total = off;
+  return p;
+}
+
+}  // namespace hhfm
+
+using namespace hhfm;
+
+extern "C" int hhfm_afm_forward_workspace(int64_t B, int32_t F, int32_t A, size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 2 || A < 1) return HHFM_EINVAL;
+  const int64_t np = (int64_t)F * (F - 1) / 2;
+  const int ntl = (A + GBN - 1) / GBN;
+  *ws_bytes = a256((size_t)B * np * ntl * 4);
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                                int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                                float w0, const float* Wt, const float* att_b,
+                                const float* att_p, int32_t A, const float* P, float* out,
+                                void* workspace, size_t ws_bytes, void* stream) {
+  if (B < 0 || F < 2 || F > 11 || k < 1 || A < 1 || features_M < 1) return HHFM_EINVAL;
+  if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
+  if (k % 4) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!idx || !E || !w || !Wt || !att_b || !att_p || !P || !out) return HHFM_EINVAL;
+  size_t need = 0;
+  hhfm_afm_forward_workspace(B, F, A, &need);
+  if (!workspace || ws_bytes < need) return HHFM_EWORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int np = F * (F - 1) / 2;
+  const int ntl = (A + GBN - 1) / GBN;
+  float* part = reinterpret_cast<float*>(workspace);
+  GemmArgs g{};
+  g.M = B * np;
+  g.N = A;
+  g.K = k;
+  g.pair_mode = 1;
+  g.P = np;
+  g.gidx = idx;
+  g.T = E;
+  g.Mtab = features_M;
+  g.F = F;
+  g.kf = k;
+  g.t_bf16 = dtype == HHFM_BF16;
+  g.Bt = Wt;
+  g.ldb = k;
+  g.bias = att_b;
+  g.relu = 1;
+  g.dotv = att_p;
+  g.partial = part;
+  launch_gemm(g, false, 1, st);
+  int64_t blocks = (B + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(afm_rows_finish, dim3((unsigned)blocks), dim3(256), 0, st, idx, B, F, E,
+                     (int)(dtype == HHFM_BF16), features_M, k, w, w0, P, part, ntl, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_afm_catalog_topk_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
+                                               int32_t item_count, int64_t max_cols,
+                                               size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 3 || k < 1 || A < 1 || item_count < 1 || max_cols < 1)
+    return HHFM_EINVAL;
+  *ws_bytes = afm_cat_plan(B, F, k, A, item_count, max_cols).total;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, const void* E,
+                                     int64_t features_M, int32_t k, int32_t dtype,
+                                     const float* w, const float* Wt, const float* att_b,
+                                     const float* att_p, int32_t A, const float* P,
+                                     int32_t item_row_begin, int32_t item_count,
+                                     int32_t global_item_base, int32_t K, int64_t max_cols,
+                                     float* top_score, int32_t* top_idx, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  if (B < 0 || F < 3 || F - 1 > kAfmMaxUF || k < 1 || k > kAfmMaxK || A < 1 ||
+      features_M < 1 || max_cols < 1)
+    return HHFM_EINVAL;
+  if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
+  if (item_count < 1 || item_row_begin < 0 || (int64_t)item_row_begin + item_count > features_M)
+    return HHFM_EINVAL;
+  if (K < 1 || K > item_count) return HHFM_EINVAL;
+  if (K > 64 || k % 4 || A % 16 || (A > 64 && A % 64)) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!qidx || !E || !w || !Wt || !att_b || !att_p || !P || !top_score || !top_idx)
+    return HHFM_EINVAL;
+  const AfmCatPlan p = afm_cat_plan(B, F, k, A, item_count, max_cols);
+  if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
+  char* ws = reinterpret_cast<char*>(workspace);
+  float* W2 = reinterpret_cast<float*>(ws + p.off_W2);
+  float* D = reinterpret_cast<float*>(ws + p.off_D);
+  float* ud = reinterpret_cast<float*>(ws + p.off_ud);
+  float* sa = reinterpret_cast<float*>(ws + p.off_sa);
+  float* part = reinterpret_cast<float*>(ws + p.off_part);
+  float* sc = reinterpret_cast<float*>(ws + p.off_sc);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int uF = F - 1;
+  const int tb = dtype == HHFM_BF16;
+  for (int64_t b0 = 0; b0 < B; b0 += p.qc) {
+    const int64_t nq = (B - b0) < p.qc ? (B - b0) : p.qc;
+    hipLaunchKernelGGL(afm_cat_prep, dim3((unsigned)nq), dim3(64), 0, st, qidx + b0 * F, nq, F,
+                       E, tb, features_M, k, Wt, att_b, att_p, A, P, W2, D, ud, sa);
+    GemmArgs g{};
+    g.M = item_count;
+    g.N = (int)(nq * uF * A);
+    g.K = k;
+    g.A = reinterpret_cast<const char*>(E) + (int64_t)item_row_begin * k * (tb ? 2 : 4);
+    g.lda = k;
+    g.a_src_bf16 = tb;
+    g.Bt = W2;
+    g.ldb = k;
+    g.bias = att_b;
+    g.relu = 1;
+    g.dotv = att_p;
+    g.partial = part;
+    g.G = p.G;
+    g.mod = A;
+    g.ldp = nq * uF * A / p.G;
+    launch_gemm(g, false, 2, st);
+    const int64_t nblk = (item_count + kWave - 1) / kWave;
+    const int64_t waves = nq * nblk;
+    hipLaunchKernelGGL(afm_cat_finish, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, nq,
+                       uF, A, p.G, part, g.ldp, D, ud, sa, E, tb, k, (int64_t)item_row_begin,
+                       item_count, w, sc);
+    int64_t tblocks = (nq + 3) / 4;
+    if (tblocks > 4096) tblocks = 4096;
+    if (K <= 32)
+      hipLaunchKernelGGL(topk_dense_kernel<32>, dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
+                         item_count, (int64_t)item_count, K, global_item_base,
+                         top_score + b0 * K, top_idx + b0 * K);
+    else
+      hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
+                         item_count, (int64_t)item_count, K, global_item_base,
+                         top_score + b0 * K, top_idx + b0 * K);
+  }
+  return (int)hipGetLastError();
+}

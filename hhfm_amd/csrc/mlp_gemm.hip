@@ -18,229 +18,9 @@
 // Epilogues: (a) relu(acc + bias) stored as bf16 / f32 (DFM.py:127-128);
 // (b) relu(acc + bias) · v summed over the tile's columns into per-row
 // partials (last hidden layer fused with the concat projection, DFM.py:137).
-#include "topk_common.h"
+#include "gemm_mfma.h"
 
 namespace hhfm {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef short bf16x8 __attribute__((ext_vector_type(8)));
-
-constexpr int GBM = 128, GBN = 128;
-
-struct GemmArgs {
-  int64_t M;
-  int N, K;
-  const void* A;       // dense A [M][lda] in compute dtype
-  int64_t lda;
-  const int32_t* gidx;  // gather mode: idx [M][F]; A[m] = concat_f T[idx[m][f]]
-  const void* T;        // table [Mtab][kf]
-  int64_t Mtab;
-  int F, kf, t_bf16;    // table row width / dtype
-  const void* Bt;       // weights, transposed: [N][ldb] (K contiguous), compute dtype
-  int64_t ldb;
-  const float* bias;    // [N] or null
-  int relu;
-  void* C;              // epilogue store: [M][ldc]
-  int64_t ldc;
-  int c_bf16;
-  const float* dotv;    // epilogue dot: v[N]
-  float* partial;       // [M][gridDim.y]
-};
-
-HHFM_DEV uint16_t f2bf(float f) {  // round to nearest even (finite inputs)
-  uint32_t u = __float_as_uint(f);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-// One 16-byte LDS chunk of A or B: 8 bf16 (bf16 mode) or 4 f32 (f32 mode).
-template <bool BF>
-struct Stage {
-  static constexpr int kElems = BF ? 8 : 4;
-  u32x4_t v;
-};
-
-// Load the 16-B chunk of A at (row m, k offset kk) in compute dtype.
-template <bool BF>
-HHFM_DEV u32x4_t load_a_chunk(const GemmArgs& g, int64_t m, int kk) {
-  u32x4_t z = {0, 0, 0, 0};
-  if (m >= g.M || kk >= g.K) return z;
-  if (!g.gidx) {
-    const char* p = reinterpret_cast<const char*>(g.A) + (m * g.lda + kk) * (BF ? 2 : 4);
-    return *reinterpret_cast<const u32x4_t*>(p);
-  }
-  const int f = kk / g.kf, c = kk - f * g.kf;
-  const int32_t id = clamp_id(g.gidx[m * g.F + f], g.Mtab);
-  if (g.t_bf16) {
-    const uint16_t* row = reinterpret_cast<const uint16_t*>(g.T) + (int64_t)id * g.kf + c;
-    if (BF) return *reinterpret_cast<const u32x4_t*>(row);   // 8 bf16
-    const uint2 x = *reinterpret_cast<const uint2*>(row);      // 4 bf16 -> 4 f32
-    u32x4_t r = {x.x << 16, x.x & 0xffff0000u, x.y << 16, x.y & 0xffff0000u};
-    return r;
-  }
-  const float* row = reinterpret_cast<const float*>(g.T) + (int64_t)id * g.kf + c;
-  if (!BF) return *reinterpret_cast<const u32x4_t*>(row);      // 4 f32
-  const float4 a = *reinterpret_cast<const float4*>(row);      // 8 f32 -> 8 bf16
-  const float4 b = *reinterpret_cast<const float4*>(row + 4);
-  u32x4_t r = {(uint32_t)f2bf(a.x) | ((uint32_t)f2bf(a.y) << 16),
-               (uint32_t)f2bf(a.z) | ((uint32_t)f2bf(a.w) << 16),
-               (uint32_t)f2bf(b.x) | ((uint32_t)f2bf(b.y) << 16),
-               (uint32_t)f2bf(b.z) | ((uint32_t)f2bf(b.w) << 16)};
-  return r;
-}
-
-template <bool BF>
-HHFM_DEV u32x4_t load_b_chunk(const GemmArgs& g, int n, int kk) {
-  u32x4_t z = {0, 0, 0, 0};
-  if (n >= g.N || kk >= g.K) return z;
-  const char* p = reinterpret_cast<const char*>(g.Bt) + ((int64_t)n * g.ldb + kk) * (BF ? 2 : 4);
-  return *reinterpret_cast<const u32x4_t*>(p);
-}
-
-template <bool BF, int EPI>
-__global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
-  constexpr int EL = BF ? 8 : 4;          // elements per 16-B chunk
-  constexpr int BK = BF ? 32 : 16;        // K per stage (= 4 chunks per row)
-  constexpr int CPR = BK / EL;            // chunks per tile row (4)
-  constexpr int LDR = CPR + 1;            // LDS row stride in chunks (+1 pad)
-  __shared__ u32x4_t As[2][GBM * LDR];
-  __shared__ u32x4_t Bs[2][GBN * LDR];
-  __shared__ float red[2][GBM];
-
-  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
-  const int wm = wv >> 1, wn = wv & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * GBM;
-  const int n0 = blockIdx.y * GBN;
-  const int nk = (g.K + BK - 1) / BK;
-
-  // each thread stages 2 A chunks and 2 B chunks per K-step
-  u32x4_t ra[2], rb[2];
-  auto gload = [&](int kt) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, r = c / CPR, p = c % CPR;
-      ra[i] = load_a_chunk<BF>(g, m0 + r, kt * BK + p * EL);
-      rb[i] = load_b_chunk<BF>(g, n0 + r, kt * BK + p * EL);
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, r = c / CPR, p = c % CPR;
-      As[buf][r * LDR + p] = ra[i];
-      Bs[buf][r * LDR + p] = rb[i];
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
-    const int ar = wm * 64 + (l & 15), br = wn * 64 + (l & 15), ch = l >> 4;
-    if constexpr (BF) {
-      // 16x16x32: lane holds A[row][8*ch .. +8], B[8*ch .. +8][col]
-      bf16x8 fa[4], fb[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const u32x4_t x = As[buf][(ar + 16 * a) * LDR + ch];
-        fa[a] = __builtin_bit_cast(bf16x8, x);
-      }
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const u32x4_t x = Bs[buf][(br + 16 * b) * LDR + ch];
-        fb[b] = __builtin_bit_cast(bf16x8, x);
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-    } else {
-      // 16x16x4 f32: lane reads k = 4*ch .. +4 and feeds MFMA j with k = 4*ch + j
-      u32x4_t fa[4], fb[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) fa[a] = As[buf][(ar + 16 * a) * LDR + ch];
-#pragma unroll
-      for (int b = 0; b < 4; ++b) fb[b] = Bs[buf][(br + 16 * b) * LDR + ch];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int b = 0; b < 4; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                __uint_as_float(fa[a][j]), __uint_as_float(fb[b][j]), acc[a][b], 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(buf ^ 1);
-    __syncthreads();
-  }
-
-  // ---- epilogue: C/D layout col = l&15, row = 4*(l>>4) + r ----
-  const int col_l = l & 15, rq = (l >> 4) * 4;
-  if constexpr (EPI == 0) {
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 64 + 16 * b + col_l;
-      const float bn = (g.bias && n < g.N) ? g.bias[n] : 0.f;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = m0 + wm * 64 + 16 * a + rq + r;
-          if (m < g.M && n < g.ldc) {
-            float v = acc[a][b][r] + bn;
-            if (g.relu) v = fmaxf(v, 0.f);
-            if (n >= g.N) v = 0.f;  // zero pad columns: next layer's K padding
-            if (g.c_bf16)
-              reinterpret_cast<uint16_t*>(g.C)[m * g.ldc + n] = f2bf(v);
-            else
-              reinterpret_cast<float*>(g.C)[m * g.ldc + n] = v;
-          }
-        }
-    }
-  } else {
-    float part[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) part[a][r] = 0.f;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int n = n0 + wn * 64 + 16 * b + col_l;
-      const bool ok = n < g.N;
-      const float bn = (ok && g.bias) ? g.bias[n] : 0.f;
-      const float vn = ok ? g.dotv[n] : 0.f;
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = acc[a][b][r] + bn;
-          if (g.relu) v = fmaxf(v, 0.f);
-          part[a][r] += ok ? v * vn : 0.f;
-        }
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = group_sum<16>(part[a][r]);
-        if (col_l == 0) red[wn][wm * 64 + 16 * a + rq + r] = s;
-      }
-    __syncthreads();
-    if (tid < GBM) {
-      const int64_t m = m0 + tid;
-      if (m < g.M) g.partial[m * gridDim.y + blockIdx.y] = red[0][tid] + red[1][tid];
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // FM part of DeepFM and the final reduce
@@ -304,61 +84,6 @@ __global__ __launch_bounds__(256) void dfm_build_rows(const int32_t* __restrict_
   }
 }
 
-// ---------------------------------------------------------------------------
-// dense top-K over materialised scores [B][N] (wave per query)
-// ---------------------------------------------------------------------------
-template <int KPAD>
-__global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict__ S,
-                                                         int64_t B, int32_t N, int64_t lds,
-                                                         int K, int32_t base,
-                                                         float* __restrict__ out_s,
-                                                         int32_t* __restrict__ out_i) {
-  const int l = lane_id();
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
-  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
-  for (int64_t b = wave; b < B; b += nwave) {
-    const float* row = S + b * lds;
-    float ls = kNegInf;
-    int32_t li = kNoIdx;
-    float thr = kNegInf;
-    for (int32_t c0 = 0; c0 < N; c0 += kWave) {
-      const int32_t i = c0 + l;
-      const float s = i < N ? row[i] : kNegInf;
-      const bool pass = i < N && s >= thr;
-      const uint64_t m = __ballot(pass);
-      const int cnt = __popcll(m);
-      if (cnt == 0) continue;
-      if (cnt > 8) {
-        float cs = pass ? s : kNegInf;
-        int32_t ci = pass ? i : kNoIdx;
-        bitonic_sort_desc<64>(cs, ci);
-        merge_lists<KPAD>(ls, li, cs, ci);
-      } else {
-        uint64_t mm = m;
-        while (mm) {
-          const int L = __builtin_ctzll(mm);
-          mm &= mm - 1;
-          const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L));
-          const int32_t ic = c0 + L;
-          const int pos = __popcll(__ballot(l < KPAD && better(ls, li, sc, ic)));
-          if (pos < K) {
-            const float ps = __shfl_up(ls, 1, kWave);
-            const int32_t pi = __shfl_up(li, 1, kWave);
-            if (l > pos) { ls = ps; li = pi; }
-            else if (l == pos) { ls = sc; li = ic; }
-          }
-        }
-      }
-      if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
-      thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1));
-    }
-    if (l < K) {
-      out_s[b * K + l] = ls;
-      out_i[b * K + l] = li == kNoIdx ? kNoIdx : li + base;
-    }
-  }
-}
-
 static void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds, int K,
                               int32_t base, float* os, int32_t* oi, hipStream_t st) {
   int64_t blocks = (B + 3) / 4;
@@ -370,17 +95,6 @@ static void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds,
   else
     hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
                        K, base, os, oi);
-}
-
-static void launch_gemm(const GemmArgs& g, bool bf, int epi, hipStream_t st) {
-  dim3 grid((unsigned)((g.M + GBM - 1) / GBM), (unsigned)((g.N + GBN - 1) / GBN));
-  if (bf) {
-    if (epi) hipLaunchKernelGGL((gemm_mfma<true, 1>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((gemm_mfma<true, 0>), grid, dim3(256), 0, st, g);
-  } else {
-    if (epi) hipLaunchKernelGGL((gemm_mfma<false, 1>), grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL((gemm_mfma<false, 0>), grid, dim3(256), 0, st, g);
-  }
 }
 
 // workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL]

@@ -18,6 +18,8 @@ using uptr = std::uintptr_t;
 
 template <typename T>
 static T* P(uptr p) { return reinterpret_cast<T*>(p); }
+template <typename T>
+static T* P_(uptr p) { return reinterpret_cast<T*>(p); }
 
 static void check(int rc, const char* what) {
   if (rc == HHFM_OK) return;
@@ -187,6 +189,53 @@ PYBIND11_MODULE(_hhfm, m) {
                                        P<void>(stream));
           }
           check(rc, "hhfm_dfm_catalog_topk");
+        });
+
+  m.def("afm_forward_workspace", [](int64_t B, int F, int A) {
+    size_t ws = 0;
+    check(hhfm_afm_forward_workspace(B, F, A, &ws), "hhfm_afm_forward_workspace");
+    return ws;
+  });
+
+  m.def("afm_forward",
+        [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w, float w0,
+           uptr Wt, uptr ab, uptr ap, int A, uptr P, uptr out, uptr ws, size_t ws_bytes,
+           uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_afm_forward(P_<const int32_t>(idx), B, F, P_<const void>(E), M, k, dtype,
+                                  P_<const float>(w), w0, P_<const float>(Wt),
+                                  P_<const float>(ab), P_<const float>(ap), A,
+                                  P_<const float>(P), P_<float>(out), P_<void>(ws), ws_bytes,
+                                  P_<void>(stream));
+          }
+          check(rc, "hhfm_afm_forward");
+        });
+
+  m.def("afm_catalog_topk_workspace",
+        [](int64_t B, int F, int k, int A, int item_count, int64_t max_cols) {
+          size_t ws = 0;
+          check(hhfm_afm_catalog_topk_workspace(B, F, k, A, item_count, max_cols, &ws),
+                "hhfm_afm_catalog_topk_workspace");
+          return ws;
+        });
+
+  m.def("afm_catalog_topk",
+        [](uptr q, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w, uptr Wt,
+           uptr ab, uptr ap, int A, uptr P, int irb, int cnt, int gbase, int K,
+           int64_t max_cols, uptr ts, uptr ti, uptr ws, size_t ws_bytes, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_afm_catalog_topk(P_<const int32_t>(q), B, F, P_<const void>(E), M, k,
+                                       dtype, P_<const float>(w), P_<const float>(Wt),
+                                       P_<const float>(ab), P_<const float>(ap), A,
+                                       P_<const float>(P), irb, cnt, gbase, K, max_cols,
+                                       P_<float>(ts), P_<int32_t>(ti), P_<void>(ws), ws_bytes,
+                                       P_<void>(stream));
+          }
+          check(rc, "hhfm_afm_catalog_topk");
         });
 
   m.def("topk_dense",

@@ -74,4 +74,59 @@ HHFM_DEV void merge_lists(float& as, int32_t& ai, float bs, int32_t bi) {
   bitonic_merge_desc<KPAD>(as, ai);
 }
 
+// ---------------------------------------------------------------------------
+// dense top-K over materialised scores [B][N] (wave per query)
+// ---------------------------------------------------------------------------
+template <int KPAD>
+__global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict__ S,
+                                                         int64_t B, int32_t N, int64_t lds,
+                                                         int K, int32_t base,
+                                                         float* __restrict__ out_s,
+                                                         int32_t* __restrict__ out_i) {
+  const int l = lane_id();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t b = wave; b < B; b += nwave) {
+    const float* row = S + b * lds;
+    float ls = kNegInf;
+    int32_t li = kNoIdx;
+    float thr = kNegInf;
+    for (int32_t c0 = 0; c0 < N; c0 += kWave) {
+      const int32_t i = c0 + l;
+      const float s = i < N ? row[i] : kNegInf;
+      const bool pass = i < N && s >= thr;
+      const uint64_t m = __ballot(pass);
+      const int cnt = __popcll(m);
+      if (cnt == 0) continue;
+      if (cnt > 8) {
+        float cs = pass ? s : kNegInf;
+        int32_t ci = pass ? i : kNoIdx;
+        bitonic_sort_desc<64>(cs, ci);
+        merge_lists<KPAD>(ls, li, cs, ci);
+      } else {
+        uint64_t mm = m;
+        while (mm) {
+          const int L = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L));
+          const int32_t ic = c0 + L;
+          const int pos = __popcll(__ballot(l < KPAD && better(ls, li, sc, ic)));
+          if (pos < K) {
+            const float ps = __shfl_up(ls, 1, kWave);
+            const int32_t pi = __shfl_up(li, 1, kWave);
+            if (l > pos) { ls = ps; li = pi; }
+            else if (l == pos) { ls = sc; li = ic; }
+          }
+        }
+      }
+      if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
+      thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1));
+    }
+    if (l < K) {
+      out_s[b * K + l] = ls;
+      out_i[b * K + l] = li == kNoIdx ? kNoIdx : li + base;
+    }
+  }
+}
+
 }  // namespace hhfm

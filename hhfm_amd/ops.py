@@ -237,3 +237,48 @@ def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0):
     native().topk_dense(scores.data_ptr(), B, N, scores.stride(0), K, global_item_base,
                         top_s.data_ptr(), top_i.data_ptr(), _stream(scores.device))
     return top_s, top_i
+
+
+# ---------------------------------------------------------------------------
+# AFM (K4)
+# ---------------------------------------------------------------------------
+def afm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, w0: float,
+                Wt: torch.Tensor, att_b: torch.Tensor, att_p: torch.Tensor, P: torch.Tensor,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """AFM.out (AFM.py:103-142) for rows ``idx`` [B, F] -> float32 [B].
+    ``Wt`` is attention_W transposed, [A, k] float32."""
+    _idx(idx, "idx")
+    dev = _need_cuda(idx, E, w, Wt, att_b, att_p, P)
+    B, F = idx.shape
+    M, k = E.shape
+    A = Wt.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.float32, device=dev)
+    nat = native()
+    ws = _workspace(dev, nat.afm_forward_workspace(B, F, A))
+    nat.afm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
+                    float(w0), Wt.data_ptr(), att_b.data_ptr(), att_p.data_ptr(), A, P.data_ptr(),
+                    out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(dev))
+    return out
+
+
+def afm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt: torch.Tensor,
+                     att_b: torch.Tensor, att_p: torch.Tensor, P: torch.Tensor,
+                     item_row_begin: int, item_count: int, K: int, global_item_base: int = 0,
+                     max_cols: int = 1 << 17):
+    """AFM.topk (AFM.py:209-246) -> (scores [B,K], ids [B,K])."""
+    _idx(qidx, "qidx")
+    dev = _need_cuda(qidx, E, w, Wt, att_b, att_p, P)
+    B, F = qidx.shape
+    M, k = E.shape
+    A = Wt.shape[0]
+    nat = native()
+    ws = _workspace(dev, nat.afm_catalog_topk_workspace(B, F, k, A, item_count, max_cols))
+    top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
+    top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
+    nat.afm_catalog_topk(qidx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
+                         Wt.data_ptr(), att_b.data_ptr(), att_p.data_ptr(), A, P.data_ptr(),
+                         item_row_begin, item_count, global_item_base, K, max_cols,
+                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), ws.numel(),
+                         _stream(dev))
+    return top_s, top_i

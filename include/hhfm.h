@@ -168,6 +168,36 @@ int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t ite
                           float* top_score, int32_t* top_idx, void* workspace,
                           size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * A1 — AFM per-row score (replaces `AFM.out`, AFM.py:103-142), attention on,
+ * keep = [1,1]: pairs i<j of the F fields, logit = Σ_a p_a·relu(((e_i⊙e_j)·W)_a
+ * + b_a), att = softmax over pairs, out = (Σ att·(e_i⊙e_j))·P + Σ w + w0.
+ * Wt: device float [A][k] = attention_W TRANSPOSED; att_b [A], att_p [A],
+ * P [k] (the prediction vector).  F <= 11, k % 4 == 0.
+ * ---------------------------------------------------------------------- */
+int hhfm_afm_forward_workspace(int64_t B, int32_t F, int32_t A, size_t* ws_bytes);
+int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                     int64_t features_M, int32_t k, int32_t dtype, const float* w, float w0,
+                     const float* Wt, const float* att_b, const float* att_p, int32_t A,
+                     const float* P, float* out, void* workspace, size_t ws_bytes,
+                     void* stream);
+
+/* A2 — AFM.topk (AFM.py:209-246): uf = [E[col 0], E[cols 2..F-1]], exp-weighted
+ * pair attention over uf pairs and uf x item pairs (raw exp, as the
+ * reference), score = (Σ_c P_c·score1_c) / weight + w_item, then top-K.
+ * At most max_cols = (queries per pass)·(F-1)·A GEMM columns per pass.
+ * k <= 256, k % 4 == 0, A % 16 == 0 (and A % 64 == 0 when A > 64), F <= 16. */
+int hhfm_afm_catalog_topk_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
+                                    int32_t item_count, int64_t max_cols,
+                                    size_t* ws_bytes);
+int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, const void* E,
+                          int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                          const float* Wt, const float* att_b, const float* att_p,
+                          int32_t A, const float* P, int32_t item_row_begin,
+                          int32_t item_count, int32_t global_item_base, int32_t K,
+                          int64_t max_cols, float* top_score, int32_t* top_idx,
+                          void* workspace, size_t ws_bytes, void* stream);
+
 /* tf.nn.top_k(scores, K) over a materialised score matrix [B][ld] (first N
  * columns), K <= 64; ids reported as global_item_base + column. */
 int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,

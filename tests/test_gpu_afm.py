@@ -1,0 +1,81 @@
+"""AFM (K4) on the GPU vs the reference graph (golden afm.npz) and vs the
+oracle at Frappe shape.  fp32 throughout (exact-fp32 MFMA); tolerance 1e-5
+of the natural magnitude of each reduction."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fm_oracle as orc
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _afm(nu, ni, M, k, A=None, F=5, table_dtype=torch.float32):
+    from hhfm_amd.AFM import AFM
+    return AFM(nu, ni, M, 1, [A or k, k], None, 0.1, 100.0, [1, 1], "AdagradOptimizer", 0.999, F,
+               table_dtype=table_dtype)
+
+
+def test_afm_vs_reference_graph():
+    d = dict(np.load(os.path.join(G, "afm.npz")))
+    nu, ni = int(d["n_user"]), int(d["n_item"])
+    M, k = d["E"].shape
+    m = _afm(nu, ni, M, k)
+    m.set_weights(feature_embeddings=d["E"], feature_bias=d["w"][:, None], bias=d["w0"],
+                  attention_W=d["attention_W"], attention_b=d["attention_b"],
+                  attention_p=d["attention_p"], prediction=d["prediction"])
+    out = m.score_rows(d["X"])[:, 0]
+    scale = np.abs(d["out"]).max()
+    assert np.allclose(out, d["out"], rtol=1e-5, atol=1e-5 * scale)
+    out2 = m.sess.run(m.out, feed_dict={m.train_features: d["X"], m.train_labels: None,
+                                         m.dropout_keep: [1.0, 1.0], m.train_phase: False})
+    assert np.array_equal(out2[:, 0], out)
+    pred = m.topk(d["A"], 20)
+    rs, ri = orc.top_k(d["topk_scores"], 21)
+    mism, amb = orc.topk_index_agreement(rs, ri[:, :20], pred,
+                                         1e-5 * np.abs(d["topk_scores"]).max(1, keepdims=True))
+    assert mism == 0, (mism, amb)
+
+
+@pytest.mark.parametrize("k,A", [(64, 64), (32, 16), (128, 128), (64, 32)])
+def test_afm_frappe_shape(k, A):
+    rng = np.random.default_rng(k + A)
+    nu, ni = 957, 4082
+    M = nu + ni + 12
+    m = _afm(nu, ni, M, k, A)
+    W = m.get_weights()
+    W["feature_bias"] = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    m.set_weights(feature_bias=W["feature_bias"])
+    X = np.stack([rng.integers(0, nu, 700), rng.integers(nu, nu + ni, 700),
+                  rng.integers(nu + ni, nu + ni + 7, 700), rng.integers(nu + ni + 7, nu + ni + 9, 700),
+                  rng.integers(nu + ni + 9, M, 700)], 1).astype(np.int32)
+    args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
+    ref = orc.afm_out(X, W["feature_embeddings"], W["feature_bias"][:, 0], 0.0, *args)[:, 0]
+    got = m.score_rows(X)[:, 0]
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    A_ = X[:40]
+    sc = orc.afm_catalog_scores(A_, W["feature_embeddings"], W["feature_bias"][:, 0], *args, nu, ni)
+    pred = m.topk(A_, 20)
+    rs, ri = orc.top_k(sc, 21)
+    mism, amb = orc.topk_index_agreement(rs, ri[:, :20], pred, 1e-5 * np.abs(sc).max(1, keepdims=True))
+    assert mism == 0, (mism, amb)
+
+
+def test_afm_catalog_query_chunks():
+    """max_cols forcing several query passes == one pass."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(1)
+    nu, ni, k = 100, 900, 32
+    M = nu + ni + 12
+    m = _afm(nu, ni, M, k)
+    A_ = np.stack([rng.integers(0, nu, 33), rng.integers(nu, nu + ni, 33),
+                   rng.integers(nu + ni, nu + ni + 7, 33), rng.integers(nu + ni + 7, nu + ni + 9, 33),
+                   rng.integers(nu + ni + 9, M, 33)], 1).astype(np.int32)
+    q = torch.from_numpy(A_).cuda()
+    Wt, b, p, P = m._att()
+    res = [ops.afm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, b, p, P,
+                                nu, ni, 20, 0, mc)[1].cpu().numpy() for mc in (1 << 17, 4 * 32 * 5)]
+    assert np.array_equal(res[0], res[1])
