@@ -238,6 +238,38 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_afm_catalog_topk");
         });
 
+  m.def("train_workspace", [](int64_t M, int k) { return hhfm_train_workspace(M, k); });
+
+  m.def("fm_train_step",
+        [](uptr idx, uptr y, int64_t B, int F, uptr E, uptr w, uptr w0, int64_t M, int k,
+           float lr, float lam, int opt, uptr accE, uptr accw, uptr accw0, uptr ws,
+           size_t ws_bytes, uptr loss, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_fm_train_step(P<const int32_t>(idx), P<const float>(y), B, F, P<float>(E),
+                                    P<float>(w), P<float>(w0), M, k, lr, lam, opt,
+                                    P<float>(accE), P<float>(accw), P<float>(accw0),
+                                    P<void>(ws), ws_bytes, P<float>(loss), P<void>(stream));
+          }
+          check(rc, "hhfm_fm_train_step");
+        });
+
+  m.def("hhfm_train_step",
+        [](uptr X, uptr Neg, int64_t B, int ncols, int c0, int c1, int t0, int t1, int NG,
+           uptr E, int64_t M, int k, float lr, float lam, int opt, uptr accE, uptr ws,
+           size_t ws_bytes, uptr loss, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_hhfm_train_step(P<const int32_t>(X), P<const int32_t>(Neg), B, ncols, c0,
+                                      c1, t0, t1, NG, P<float>(E), M, k, lr, lam, opt,
+                                      P<float>(accE), P<void>(ws), ws_bytes, P<float>(loss),
+                                      P<void>(stream));
+          }
+          check(rc, "hhfm_hhfm_train_step");
+        });
+
   m.def("topk_dense",
         [](uptr scores, int64_t B, int N, int64_t ld, int K, int base, uptr top_score,
            uptr top_idx, uptr stream) {

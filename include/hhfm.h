@@ -198,6 +198,30 @@ int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, const void*
                           int64_t max_cols, float* top_score, int32_t* top_idx,
                           void* workspace, size_t ws_bytes, void* stream);
 
+/* ------------------------------------------------------------------------
+ * H6 — one training step (`partial_fit`, sess.run((loss, optimizer))).
+ *   FM   (FM.py:123-136):        loss = Σ (y − out)²/2 + λ·Σ E²/2
+ *   HHFM (OurModel7.py:172-193): loss = −Σ log σ(pos − max_j neg_j) + λ·Σ E²/2
+ * optimizer 0 = TF AdagradOptimizer (accumulators initialised to 0.1 by the
+ * caller; accum += g², var -= lr·g·rsqrt(accum)), 1 = GradientDescent.
+ * E, w are fp32 and updated in place; *loss (device float) receives the loss
+ * of the pre-update parameters.  The workspace (hhfm_train_workspace bytes)
+ * must be zero-filled once; the step leaves it zeroed.  HHFM: X [B][ncols]
+ * full rows [user, item, ctx..., time...], Neg [B][NG] negative item ids,
+ * NG <= 16.
+ * ---------------------------------------------------------------------- */
+size_t hhfm_train_workspace(int64_t features_M, int32_t k);
+int hhfm_fm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F, float* E,
+                       float* w, float* w0, int64_t features_M, int32_t k, float lr,
+                       float lambda_l2, int32_t optimizer, float* accE, float* accw,
+                       float* accw0, void* workspace, size_t ws_bytes, float* loss,
+                       void* stream);
+int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_t B, int32_t ncols,
+                         int32_t ctx_begin, int32_t ctx_end, int32_t time_begin,
+                         int32_t time_end, int32_t NG, float* E, int64_t features_M,
+                         int32_t k, float lr, float lambda_l2, int32_t optimizer, float* accE,
+                         void* workspace, size_t ws_bytes, float* loss, void* stream);
+
 /* tf.nn.top_k(scores, K) over a materialised score matrix [B][ld] (first N
  * columns), K <= 64; ids reported as global_item_base + column. */
 int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,

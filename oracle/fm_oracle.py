@@ -273,3 +273,80 @@ def dfm_catalog_rows(A, n_user, n_item):
 def dfm_catalog_scores(A, E, w, layers, biases, Wp, bp, n_user, n_item):
     rows = dfm_catalog_rows(A, n_user, n_item)
     return dfm_out(rows, E, w, layers, biases, Wp, bp).reshape(-1, n_item)  # :228
+
+
+# ---------------------------------------------------------------------------
+# H6 — one training step with TF-1.x semantics (loss + gradient + optimizer)
+# ---------------------------------------------------------------------------
+def tf_adagrad(var, grad, acc, lr):
+    """tf.train.AdagradOptimizer (ApplyAdagrad): accum += g²; var -= lr·g·rsqrt(accum).
+    Accumulators start at initial_accumulator_value = 0.1 (TF default)."""
+    acc = (acc + grad * grad).astype(F32)
+    return (var - F32(lr) * grad / np.sqrt(acc)).astype(F32), acc
+
+
+def fm_train_step(X, y, E, w, w0, accE, accw, accw0, lr, lam, optimizer="adagrad"):
+    """FM partial_fit (FM.py:123-136, 168-171): loss = Σ(y−out)²/2 + λ·ΣE²/2.
+    Returns (loss, E, w, w0, accE, accw, accw0) after one update."""
+    X = np.asarray(X, np.int64)
+    y = np.asarray(y, F32).reshape(-1)
+    E = np.asarray(E, F32)
+    w = np.asarray(w, F32).reshape(-1)
+    out = fm_out(X, E, w, w0)[:, 0]
+    r = y - out
+    loss = F32(np.sum(r * r, dtype=np.float64) / 2 + lam * np.sum(E.astype(np.float64) ** 2) / 2)
+    g = -r                                                     # d loss / d out
+    e = E[X]
+    s = e.sum(1)
+    dE = np.zeros_like(E)
+    for f in range(X.shape[1]):
+        np.add.at(dE, X[:, f], g[:, None] * (s - e[:, f]))     # ∂out/∂e_f = Σe − e_f
+    dE += F32(lam) * E                                         # l2_regularizer
+    dw = np.zeros_like(w)
+    for f in range(X.shape[1]):
+        np.add.at(dw, X[:, f], g)
+    dw0 = F32(g.sum())
+    if optimizer == "adagrad":
+        E, accE = tf_adagrad(E, dE, accE, lr)
+        w, accw = tf_adagrad(w, dw, accw, lr)
+        w0n, accw0 = tf_adagrad(np.float32(w0), dw0, np.float32(accw0), lr)
+    else:
+        E, w, w0n = E - F32(lr) * dE, w - F32(lr) * dw, F32(w0) - F32(lr) * dw0
+    return loss, E, w, F32(w0n), accE, accw, accw0
+
+
+def hhfm_train_step(X, Neg, E, accE, lr, lam, feature_dimension, time_dimension,
+                    context=True, time=False, optimizer="adagrad"):
+    """OUR partial_fit (OurModel7.py:171-193): loss = −Σ log σ(pos − max_j neg_j)
+    + λ·ΣE²/2; reduce_max's gradient is split equally between tied maxima."""
+    X = np.asarray(X, np.int64)
+    Neg = np.asarray(Neg, np.int64)
+    E = np.asarray(E, F32)
+    ctx, tim = hhfm_split(X, feature_dimension, time_dimension, context, time)
+    h = _hybrid(E, X[:, 0], ctx, tim)
+    it = E[X[:, 1]]
+    pos = (h * it).sum(1, dtype=F32)
+    neg = (h[:, None, :] * E[Neg]).sum(2, dtype=F32)
+    mx = neg.max(1)
+    z = pos - mx
+    sg = (1.0 / (1.0 + np.exp(-z))).astype(F32)
+    loss = F32(-np.sum(np.log(sg), dtype=np.float64) + lam * np.sum(E.astype(np.float64) ** 2) / 2)
+    g = sg - F32(1)
+    ind = (neg == mx[:, None]).astype(F32)
+    ind /= ind.sum(1, keepdims=True)
+    dh = g[:, None] * (it - (ind[:, :, None] * E[Neg]).sum(1))
+    dE = np.zeros_like(E)
+    np.add.at(dE, X[:, 1], g[:, None] * h)
+    for j in range(Neg.shape[1]):
+        np.add.at(dE, Neg[:, j], -(g * ind[:, j])[:, None] * h)
+    np.add.at(dE, X[:, 0], dh)
+    for cols in (ctx, tim):
+        if cols is not None:
+            for c in range(cols.shape[1]):
+                np.add.at(dE, np.asarray(cols)[:, c].astype(np.int64), dh)
+    dE += F32(lam) * E
+    if optimizer == "adagrad":
+        E, accE = tf_adagrad(E, dE, accE, lr)
+    else:
+        E = E - F32(lr) * dE
+    return loss, E, accE

@@ -1,0 +1,107 @@
+"""H6 on the GPU: partial_fit steps vs the oracle's TF-semantics step
+(hand-derived gradients pinned by finite differences in
+tests/test_oracle_training.py), and the reference epoch loops end to end.
+Gradients are summed with float atomics, so updates agree to ~1e-6
+relative, not bitwise."""
+import argparse
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fm_oracle as orc
+
+pytestmark = pytest.mark.gpu
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _rows(rng, B, nu, ni, ctx, td=0):
+    cols = [rng.integers(0, nu, B), rng.integers(nu, nu + ni, B)]
+    o = nu + ni
+    for c in ctx:
+        cols.append(rng.integers(o, o + c, B))
+        o += c
+    for _ in range(td):
+        cols.append(rng.integers(nu, nu + ni, B))
+    return np.stack(cols, 1).astype(np.int64), o
+
+
+@pytest.mark.parametrize("opt", ["AdagradOptimizer", "GradientDescentOptimizer"])
+def test_fm_partial_fit_matches_oracle(opt):
+    from hhfm_amd.FM import FM
+    rng = np.random.default_rng(0)
+    nu, ni, k = 200, 500, 32
+    X, M = _rows(rng, 5000, nu, ni, (7, 2, 3))
+    m = FM(5, M, nu, ni, k, 0.1, 0.1, 1, opt, 0, 0)
+    E = rng.normal(0, 0.01, (M, k)).astype(np.float32)
+    w = rng.normal(0, 0.01, M).astype(np.float32)
+    m.set_weights(feature_embeddings=E, feature_bias=w[:, None], bias=np.float32(0.02))
+    accE, accw, acc0 = np.full_like(E, 0.1), np.full_like(w, 0.1), np.float32(0.1)
+    w0 = np.float32(0.02)
+    o = "adagrad" if opt == "AdagradOptimizer" else "sgd"
+    for step in range(3):
+        Xb = X[step * 1500:(step + 1) * 1500]
+        y = rng.integers(0, 2, len(Xb)).astype(np.float32)[:, None]
+        loss = m.partial_fit({"X": Xb, "Y": y})
+        rl, E1, w1, w01, accE, accw, acc0 = orc.fm_train_step(Xb, y, E, w, w0, accE, accw, acc0,
+                                                              0.1, 0.1, o)
+        assert np.isclose(loss, rl, rtol=1e-5)
+        Wg = m.get_weights()
+        assert np.allclose(Wg["feature_embeddings"] - E, E1 - E, rtol=1e-4, atol=1e-7)
+        assert np.allclose(Wg["feature_bias"][:, 0] - w, w1 - w, rtol=1e-4, atol=1e-7)
+        assert np.isclose(float(Wg["bias"]), w01, rtol=1e-5, atol=1e-7)
+        E, w, w0 = E1, w1, w01
+
+
+@pytest.mark.parametrize("layout", ["frappe", "jiaju"])
+def test_hhfm_partial_fit_matches_oracle(layout):
+    from hhfm_amd.OurModel7 import OUR
+    rng = np.random.default_rng(1)
+    nu, ni, k = 300, 800, 32
+    ctx, td = ((7, 2, 3), 0) if layout == "frappe" else ((5, 4, 6, 3, 7), 3)
+    X, M = _rows(rng, 3000, nu, ni, ctx, td)
+    fd = len(ctx)
+    m = OUR(fd, td, M, nu, ni, k, 0.1, 0.01, "AdagradOptimizer", True, td > 0)
+    E = rng.normal(0, 0.01, (M, k)).astype(np.float32)
+    m.set_weights(feature_embeddings=E)
+    accE = np.full_like(E, 0.1)
+    for step in range(2):
+        Xb = X[step * 1500:(step + 1) * 1500]
+        Neg = rng.integers(nu, nu + ni, (len(Xb), 10))
+        data = {"X": Xb[:, :2], "Y": Neg, "F1": Xb[:, 2:2 + fd]}
+        if td:
+            data["F2"] = Xb[:, 2 + fd:]
+        loss = m.partial_fit(data)
+        rl, E1, accE = orc.hhfm_train_step(Xb, Neg, E, accE, 0.1, 0.01, fd, td, True, td > 0)
+        assert np.isclose(loss, rl, rtol=1e-5)
+        got = m.get_weights()["feature_embeddings"]
+        assert np.allclose(got - E, E1 - E, rtol=1e-4, atol=1e-7)
+        E = E1
+
+
+def _args(tmp_path, **kw):
+    a = dict(path=G + "/", dataset="synth_frappe", epoch=3, batch_size=5000, hidden_factor=32,
+             lamda=0.1, keep=1, lr=0.1, optimizer="AdagradOptimizer", verbose=1, batch_norm=0,
+             TopK=10, Result=0, result_file=str(tmp_path / "result.txt"))
+    a.update(kw)
+    return argparse.Namespace(**a)
+
+
+def test_fm_train_loop_end_to_end(tmp_path):
+    from hhfm_amd.FM import Train
+    np.random.seed(2016)
+    t = Train(_args(tmp_path))
+    losses = t.train()
+    assert len(losses) == 2 and losses[1] < losses[0]
+    log = open(tmp_path / "result.txt").read()
+    assert "Init" in log and "FM Epoch 1" in log
+
+
+def test_hhfm_train_loop_end_to_end(tmp_path):
+    from hhfm_amd.OurModel7 import Train
+    np.random.seed(2016)
+    t = Train(_args(tmp_path, lamda=0.01, epoch=11))
+    losses = t.train()
+    assert len(losses) == 10 and losses[-1] < losses[0]
+    assert "M7 Epoch 10" in open(tmp_path / "result.txt").read()

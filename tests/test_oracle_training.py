@@ -1,0 +1,73 @@
+"""The oracle's hand-written TF gradients (H6) vs finite differences of the
+oracle's own loss (float64), and TF Adagrad semantics."""
+import numpy as np
+
+from oracle import fm_oracle as orc
+
+
+def _fd(loss_fn, E, ids, eps=1e-3):
+    E = E.astype(np.float64)
+    out = []
+    for (r, c) in ids:
+        Ep, Em = E.copy(), E.copy()
+        Ep[r, c] += eps
+        Em[r, c] -= eps
+        out.append((loss_fn(Ep) - loss_fn(Em)) / (2 * eps))
+    return np.array(out)
+
+
+def test_fm_gradient_matches_finite_differences():
+    rng = np.random.default_rng(0)
+    M, k, B, lam = 30, 4, 20, 0.1
+    X = rng.integers(0, M, size=(B, 5))
+    X[0, 3] = X[0, 2]                       # repeated id inside one row
+    y = rng.integers(0, 2, B).astype(np.float64)
+    E = rng.normal(0, 0.3, (M, k))
+    w = rng.normal(0, 0.3, M)
+
+    def loss(Ev):
+        e = Ev[X]
+        s = e.sum(1)
+        out = (0.5 * (s * s - (e * e).sum(1))).sum(1) + w[X].sum(1)
+        return ((y - out) ** 2).sum() / 2 + lam * (Ev ** 2).sum() / 2
+
+    lr = 1e-3
+    _, E1, *_ = orc.fm_train_step(X, y, E.astype(np.float32), w, 0.0, np.zeros((M, k), np.float32),
+                                  np.zeros(M, np.float32), 0.0, lr, lam, optimizer="sgd")
+    grad = (E.astype(np.float32) - E1) / lr
+    ids = [(X[0, 2], 1), (X[3, 0], 0), (X[5, 4], 3), (int(np.setdiff1d(np.arange(M), X)[0]), 2)]
+    fd = _fd(loss, E, ids)
+    got = np.array([grad[r, c] for r, c in ids])
+    assert np.allclose(got, fd, rtol=2e-3, atol=2e-4)
+
+
+def test_hhfm_gradient_matches_finite_differences():
+    rng = np.random.default_rng(1)
+    M, k, B, lam = 40, 4, 12, 0.01
+    X = np.stack([rng.integers(0, 10, B), rng.integers(10, 30, B), rng.integers(30, 35, B),
+                  rng.integers(35, 40, B)], 1)
+    Neg = rng.integers(10, 30, size=(B, 10))
+    E = rng.normal(0, 0.5, (M, k))
+
+    def loss(Ev):
+        h = Ev[X[:, 0]] + Ev[X[:, 2:]].sum(1)
+        pos = (h * Ev[X[:, 1]]).sum(1)
+        neg = (h[:, None, :] * Ev[Neg]).sum(2)
+        z = pos - neg.max(1)
+        return -np.log(1 / (1 + np.exp(-z))).sum() + lam * (Ev ** 2).sum() / 2
+
+    lr = 1e-3
+    _, E1, _ = orc.hhfm_train_step(X, Neg, E.astype(np.float32), np.zeros((M, k), np.float32), lr,
+                                   lam, 2, 0, optimizer="sgd")
+    grad = (E.astype(np.float32) - E1) / lr
+    ids = [(X[0, 0], 1), (X[1, 1], 2), (X[2, 2], 0), (Neg[0, 3], 3), (X[4, 3], 1)]
+    fd = _fd(loss, E, ids, eps=1e-4)
+    got = np.array([grad[r, c] for r, c in ids])
+    assert np.allclose(got, fd, rtol=3e-3, atol=3e-4)
+
+
+def test_tf_adagrad_semantics():
+    v, g, a = np.float32([1.0]), np.float32([0.5]), np.float32([0.1])
+    v1, a1 = orc.tf_adagrad(v, g, a, 0.1)
+    assert a1[0] == np.float32(0.35)
+    assert np.isclose(v1[0], 1.0 - 0.1 * 0.5 / np.sqrt(0.35))
