@@ -47,6 +47,10 @@ def parse():
                    help="CPU-baseline time budget (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 21)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
+    p.add_argument("--legs", default="hr,catalog",
+                   help="extra legs: hr (HR@10 identity after GPU training on Frappe-shape "
+                        "data), catalog (C4 item-sharded top-K, RCCL all-gather at N>1)")
+    p.add_argument("--hr-epochs", type=int, default=5)
     return p.parse_args()
 
 
@@ -104,6 +108,126 @@ def cpu_baseline(idx, E, w, w0, out_gpu, args):
             "sample": f"{n} rows of the same workload (same 4.3 GB table) x {reps} passes, "
                       f"oracle/cpu_oracle.c (OpenMP) on {cpu_name}",
             "gpu_vs_cpu_max_rel_err": err}
+
+
+def frappe_shape_dataset(path, rows=96203, seed=11):
+    """A synthetic libfm file with Frappe's shape: 957 users, 4082 items,
+    daytime/isweekend/homework with 7/2/3 values, 96,203 rows, popularity
+    skew (no Frappe rows are used or shipped)."""
+    rng = np.random.default_rng(seed)
+    os.makedirs(os.path.join(path, "frappe_shape"), exist_ok=True)
+    fn = os.path.join(path, "frappe_shape", "frappe_shape.libfm")
+    users = rng.zipf(1.3, rows) % 957
+    pref = rng.integers(0, 4082, 957)            # each user's taste centre
+    items = (pref[users] + (rng.zipf(1.4, rows) % 4082) * rng.choice([-1, 1], rows)) % 4082
+    day = rng.integers(0, 7, rows)
+    wk = rng.integers(0, 2, rows)
+    hw = rng.integers(0, 3, rows)
+    with open(fn, "w") as f:
+        for u, i, d, w_, h in zip(users, items, day, wk, hw):
+            f.write(f"1 u{u} i{i} d{d} w{w_} h{h}\n")
+    return path + "/"
+
+
+def hr_leg(dev, epochs):
+    """Load -> train HHFM (k=64, the reference hyper-parameters) on the GPU ->
+    evaluate_TopK(TopK=10) with the GPU model and with the oracle model holding
+    the same weights and the same sampled rows: HR@10 must be identical."""
+    import tempfile
+    from hhfm_amd.NewLoadData import LoadData
+    from hhfm_amd.OurModel7 import OUR
+    from hhfm_amd.harness import Train
+    from hhfm_amd import training
+    from oracle import fm_oracle as orc
+
+    class _Oracle:
+        def __init__(self, E, nu, ni):
+            self.E, self.nu, self.ni = E, nu, ni
+
+        def score_rows(self, X):
+            return orc.hhfm_positive_feedback(X, self.E, 3, 0)
+
+        def topk(self, A, tp):
+            return orc.hhfm_topk(A, self.E, self.nu, self.ni, 3, 0, tp=tp)[1]
+
+    t0 = time.perf_counter()
+    with tempfile.TemporaryDirectory() as tmp:
+        np.random.seed(2016)
+        data = LoadData(frappe_shape_dataset(tmp), "frappe_shape")
+    m = OUR(3, 0, data.features_M, data.n_user, data.n_item, 64, 0.1, 0.01, "AdagradOptimizer",
+            True, False, device=dev)
+    tr = Train(data=data, model=m)
+    tr.batch_size, tr.epoch, tr.TopK = 5000, epochs + 1, 10
+    tr.context, tr.time, tr.time_dimension = True, False, 0
+    tr.args = argparse.Namespace(Result=-1, result_file=None, dataset="frappe_shape")
+    losses = training.run_training_hhfm(tr)
+    t_train = time.perf_counter() - t0
+    res = {}
+    for name, model in (("gpu", m), ("oracle", _Oracle(m.get_weights()["feature_embeddings"],
+                                                       data.n_user, data.n_item))):
+        tr.model = model
+        np.random.seed(2024)
+        res[name] = [float(x) for x in tr.evaluate_TopK(data.Test_data)]
+    return {"hr10": res["gpu"][0], "ndcg10": res["gpu"][1], "pre10": res["gpu"][2],
+            "oracle_hr10": res["oracle"][0], "identical_to_oracle": res["gpu"] == res["oracle"],
+            "data": "Frappe-shape synthetic (957 users, 4082 items, ctx 7/2/3, 96,203 rows), "
+                    "LoadData split seed 2016",
+            "model": f"HHFM k=64 trained {epochs} epochs on the GPU (partial_fit kernels), "
+                     "evaluate_TopK TopK=10 (3000 rows)",
+            "epoch_loss": losses, "train_s": t_train}
+
+
+def catalog_leg(dev, world, rank, reps=5):
+    """C4: HHFM k=128, 1 M users, 10 M items sharded contiguously over the
+    ranks, 1,024 queries, K=20, fp32; local hhfm_catalog_topk + RCCL
+    all-gather + hhfm_topk_merge per step."""
+    from hhfm_amd import distributed as hd
+    from hhfm_amd import ops
+    nu, ni, k, B, K = 1 << 20, 10_000_000, 128, 1024, 20
+    begin, end = hd.shard_range(ni, world, rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    # replicated users + ctx, only this rank's item rows are materialised
+    rows_user = torch.empty(nu, k, device=dev).normal_(0, 0.01, generator=g)
+    rows_ctx = torch.empty(12, k, device=dev).normal_(0, 0.01, generator=g)
+    gi = torch.Generator(device=dev)
+    gi.manual_seed(1000 + rank)
+    rows_item = torch.empty(end - begin, k, device=dev).normal_(0, 0.01, generator=gi)
+    E = torch.cat([rows_user, rows_item, rows_ctx]).contiguous()
+    del rows_user, rows_item
+    off = nu + (end - begin)
+    cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
+            torch.zeros(B, dtype=torch.int64, device=dev)]
+    for c in (7, 2, 3):
+        cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+        off += c
+    A = torch.stack(cols, 1).to(torch.int32).contiguous()
+
+    def scorer(A_, b0, cnt, Kl):
+        return ops.catalog_topk(A_, E, ops.MODE_HHFM, Kl, nu, cnt, b0, None, 0, (2, 5), (0, 0))
+
+    def step():
+        return hd.sharded_topk(A, K, ni, scorer)
+
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        s, i = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    ms = float(el[0]) / reps * 1e3
+    pairs = B * ni
+    return {"workload": "C4: HHFM k=128 fp32, 10M-item catalog sharded over ranks, "
+                        "1,024 queries, top-20 (local MFMA score+select, RCCL all-gather, merge)",
+            "ms_per_query_batch": ms, "pairs_per_s": pairs / (ms * 1e-3),
+            "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world}
 
 
 def main():
@@ -177,6 +301,17 @@ def main():
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(idx, E, w, w0, out, args)
+    legs = [x for x in args.legs.split(",") if x]
+    del idx, E, w, out
+    torch.cuda.empty_cache()
+    extra = {}
+    if "catalog" in legs:
+        extra["catalog_c4"] = catalog_leg(dev, world, rank)
+        torch.cuda.empty_cache()
+    if "hr" in legs and rank == 0:
+        extra["hr_at_10"] = hr_leg(dev, args.hr_epochs)
+    if extra:
+        result["extra"] = extra
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
