@@ -279,8 +279,9 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("rows") == args.rows and tj.get("k") == args.k:
-                traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("k") == args.k and tj.get("fields") == 5:
+                # PMC bytes per row (calibrated FETCH_SIZE + WRITE_SIZE) x rows per launch
+                traffic = tj["hbm_bytes_per_row"] * args.rows
         except (OSError, ValueError):
             traffic = None
 

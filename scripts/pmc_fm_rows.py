@@ -7,7 +7,9 @@ Two launches of the headline kernel on the bench table (16.8 M x 64 fp32):
      once, so its HBM read bytes are known (B*(2*256+20+8)) and calibrate
      FETCH_SIZE for this access pattern (MI355X_MICROARCH.md §HBM: gfx950
      FETCH_SIZE under-counts wide coalesced reads by 2x);
-  2. `bench`: the bench.py workload (uniform random ids), same B.
+  2. `bench`: the bench.py workload (uniform random ids), same B;
+  3. `bench without w`: same rows with the bias gathers removed (isolates
+     the cost of the two 4-byte w gathers per row).
 Run under: rocprofv3 --pmc FETCH_SIZE ... -- python scripts/pmc_fm_rows.py
            rocprofv3 --pmc WRITE_SIZE ... -- python scripts/pmc_fm_rows.py
 """
@@ -30,8 +32,9 @@ r = torch.arange(rows, device=dev, dtype=torch.int32)
 seq[:, 0] = r % (8 << 20)
 seq[:, 1] = (8 << 20) + r % (8 << 20)
 torch.cuda.synchronize()
-# two launches each; rocprof reports one row per dispatch (order: calib, calib, bench, bench)
-for x in (seq, seq, idx, idx):
-    ops.fm_score_rows(x, E, w, 0.0, out=out)
+# two launches each; rocprof reports one row per dispatch, in order:
+# calib, calib, bench, bench, bench-without-w, bench-without-w
+for x, ww in ((seq, w), (seq, w), (idx, w), (idx, w), (idx, None), (idx, None)):
+    ops.fm_score_rows(x, E, ww, 0.0, out=out)
 torch.cuda.synchronize()
 print("pmc workload done", rows)
