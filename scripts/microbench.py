@@ -78,4 +78,63 @@ if not only or "k2" in only:
                      "pairs_per_s": B * ni / (med * 1e-3)}
         del E
         torch.cuda.empty_cache()
+if not only or "dfm" in only:
+    # C5 per-GPU shape (DFM k=256, 3x400 MLP, Frappe-field rows), 2 M rows per launch
+    from hhfm_amd.DFM import DeepFM
+    nu, ni = 957, 4082
+    M = nu + ni + 12
+    B = 1 << 21
+    g = torch.Generator(device=dev)
+    g.manual_seed(4)
+    cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
+            torch.randint(nu, nu + ni, (B,), generator=g, device=dev)]
+    off = nu + ni
+    for c in (7, 2, 3):
+        cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+        off += c
+    X = torch.stack(cols, 1).to(torch.int32).contiguous()
+    flops_row = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
+    for mdt, name in ((torch.bfloat16, "dfm_c5_bf16"), (torch.float32, "dfm_c5_f32")):
+        m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
+                   mlp_dtype=mdt)
+        m.validate = False
+        Wt, bs, dims, Wp, bp = m._prepared()
+        out = torch.empty(B, device=dev)
+        fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,  # noqa
+                                     dims, mdt, Wp, bp, out=out)
+        med, mn = timeit(fn, reps=5)
+        res[name] = {"median_ms": med, "rows_per_s": B / (med * 1e-3),
+                     "TFLOPs": flops_row * B / (med * 1e-3) / 1e12}
+        del m
+        torch.cuda.empty_cache()
+
+if not only or "afm" in only:
+    from hhfm_amd.AFM import AFM
+    nu, ni, k = 957, 4082, 64
+    M = nu + ni + 12
+    m = AFM(nu, ni, M, 1, [k, k], None, 0.1, 100.0, [1, 1], "AdagradOptimizer", 0.999, 5,
+            device=dev)
+    m.validate = False
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    B = 1 << 20
+    cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
+            torch.randint(nu, nu + ni, (B,), generator=g, device=dev)]
+    off = nu + ni
+    for c in (7, 2, 3):
+        cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+        off += c
+    X = torch.stack(cols, 1).to(torch.int32).contiguous()
+    Wt, b, p_, P = m._att()
+    out = torch.empty(B, device=dev)
+    med, mn = timeit(lambda: ops.afm_forward(X, m.table, m.weights["feature_bias"].reshape(-1),
+                                             0.0, Wt, b, p_, P, out=out), reps=5)
+    res["afm_rows_k64"] = {"median_ms": med, "rows_per_s": B / (med * 1e-3),
+                           "TFLOPs": 2.0 * 10 * k * k * B / (med * 1e-3) / 1e12}
+    A = X[:300]
+    med, mn = timeit(lambda: ops.afm_catalog_topk(A, m.table, m.weights["feature_bias"].reshape(-1),
+                                                  Wt, b, p_, P, nu, ni, 20), reps=5)
+    res["afm_topk_c300_k64"] = {"median_ms": med,
+                                "TFLOPs": 2.0 * 300 * ni * 4 * k * k / (med * 1e-3) / 1e12}
+
 print(json.dumps(res, indent=1))
