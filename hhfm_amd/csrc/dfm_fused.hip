@@ -1,0 +1,405 @@
+// K3' — DeepFM forward as ONE kernel per 128-row block (bf16 MLP).
+//
+//   Used by hhfm_dfm_forward / hhfm_dfm_catalog_topk (mlp_gemm.hip) when the
+//   MLP runs in bf16, k % 16 == 0, k <= 512, F <= 16, at most 4 layers and
+//   every layer at most 416 wide; otherwise the layer-by-layer GEMM path runs.
+//   Replaces DeepFM.out (Newcode/DFM.py:104-137) end to end.
+//
+// Why: the layered path re-gathers the [B, F·k] operand once per 128-column
+// tile and round-trips every activation through HBM.  Here a wave owns 32
+// rows for the whole network and keeps them in registers:
+//
+//   * every layer computes the TRANSPOSED product  Yᵀ[n][m] = W[n][:]·Xᵀ[:][m]
+//     with v_mfma_f32_32x32x16_bf16 (A = weight rows from LDS, B = the
+//     wave's activations), so a result tile has the row m on the lane and
+//     the output features n in its 16 registers;
+//   * the epilogue (bias, ReLU, bf16 RNE) packs those registers pairwise and
+//     one v_permlane32_swap per pair puts them in the next layer's B-operand
+//     order (k = 8·half + j) — activations never touch LDS or HBM;
+//   * layer 0's B operand is gathered straight from the embedding table into
+//     registers one K-chunk ahead, in c-major order (all F fields of one
+//     16-column slice in a row), so the same values also give the FM part
+//     ½((Σe)²−Σe²)·Wp and the output needs no second pass over E;
+//   * dfm_pack_weights first lays all weights out as a sequence of 64-deep
+//     K-chunks, each [32·TM rows][8 × 16 B] zero-padded, in the layer-0 step
+//     order and already XOR-swizzled, so a chunk is ONE contiguous block:
+//     the main kernel streams chunk g+1 into the other half of a double
+//     buffer by LDS-DMA (global_load_lds_dwordx4, lane-linear) while the
+//     block's 4 waves run chunk g's MFMAs (one barrier a chunk).
+//
+// All LDS is one __shared__ object: a second object beside the LDS-DMA
+// target makes hipcc drain the DMA (vmcnt(0)) before LDS reads.
+//
+// out[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c]) + bp) + Σ_n relu(h_L)·Wp[F+k+n]
+#include "gemm_mfma.h"
+
+namespace hhfm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int kFusedMaxLayers = 4;
+constexpr int kFusedMaxF = 16;
+constexpr int kFusedMaxK = 512;
+constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
+constexpr int kFusedMaxSteps = kFusedMaxF * kFusedMaxK / 16 + 4;
+
+struct FusedDfmArgs {
+  const int32_t* idx;
+  int64_t B;
+  int F, k;
+  const void* E;
+  int64_t M;
+  const float* w;
+  int L;
+  int dims[kFusedMaxLayers];
+  int ldb[kFusedMaxLayers];
+  const uint16_t* Wt[kFusedMaxLayers];
+  const float* bias[kFusedMaxLayers];
+  const float* Wp;
+  float bp;
+  float* out;
+  const uint4* packed;   // chunk sequence written by dfm_pack_weights
+};
+
+HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+HHFM_DEV void swap_halves(uint32_t& a, uint32_t& b) {
+  // lanes 32-63 of a <-> lanes 0-31 of b
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+
+// Chunk g, row n, slot u' holds 8 bf16 of source unit u = u' ^ ((n>>1)&7):
+//   layer 0, chunk c:  step S = 4c + u/2 -> W0[n][(S%F)·k + 16(S/F) + 8(u&1) ..]
+//   layer i, chunk c:  Wi[n][64c + 8u ..]
+// zero outside the layer's rows / columns / steps.
+__global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, int nc0, int NC,
+                                                        uint4* __restrict__ out) {
+  const int NR = 32 * TM;
+  const int nS = a.F * (a.k / 16);
+  const int64_t total = (int64_t)(nc0 + (a.L - 1) * NC) * NR * 8;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(x / (NR * 8));
+    const int rem = (int)(x - (int64_t)g * NR * 8);
+    const int n = rem >> 3, u = (rem & 7) ^ ((n >> 1) & 7);
+    int i, kk;
+    bool ok;
+    if (g < nc0) {
+      i = 0;
+      const int S = 4 * g + (u >> 1);
+      ok = S < nS;
+      kk = (S % a.F) * a.k + 16 * (S / a.F) + 8 * (u & 1);
+    } else {
+      i = 1 + (g - nc0) / NC;
+      kk = 64 * ((g - nc0) % NC) + 8 * u;
+      ok = kk < a.ldb[i];
+    }
+    ok = ok && n < a.dims[i];
+    out[x] = ok ? *reinterpret_cast<const uint4*>(a.Wt[i] + (int64_t)n * a.ldb[i] + kk)
+                : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <bool TBF, int TM>
+__global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
+  constexpr int NR = TM * 32;                // weight rows per chunk
+  constexpr int CU = NR * 8;                 // 16-B units per chunk
+  constexpr int NC = (TM + 1) / 2;           // chunks per hidden layer
+  constexpr int kW = 2 * CU * 16;
+  constexpr int kIds = kW, kBl = kIds + kFusedRows * kFusedMaxF * 4;
+  constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
+  constexpr int kSf = kWp + (kFusedMaxF + kFusedMaxK) * 4, kSc = kSf + kFusedMaxSteps * 4;
+  constexpr int kSmem = kSc + kFusedMaxSteps * 4;
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+  uint4* wbuf0 = reinterpret_cast<uint4*>(smem);   // [2][NR rows][8 slots]
+  int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
+  float* blv = reinterpret_cast<float*>(smem + kBl);  // [layer][NR]
+  float* vl = reinterpret_cast<float*>(smem + kVl);
+  float* wpl = reinterpret_cast<float*>(smem + kWp);
+  int32_t* step_f = reinterpret_cast<int32_t*>(smem + kSf);
+  int32_t* step_col = reinterpret_cast<int32_t*>(smem + kSc);
+
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int r = l & 31, h = l >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * kFusedRows;
+  const int F = a.F, k = a.k, L = a.L;
+  const int nS = F * (k / 16);               // layer-0 k16 steps
+  const int nc0 = (nS + 3) / 4;              // layer-0 K-chunks
+  const int nchunks = nc0 + (L - 1) * NC;
+
+  for (int x = tid; x < kFusedRows * F; x += 256) {
+    const int64_t m = m0 + x / F;
+    ids[x] = m < a.B ? clamp_id(a.idx[m * F + x % F], a.M) : 0;
+  }
+  for (int i = 0; i < L; ++i)
+    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
+  for (int x = tid; x < F + k; x += 256) wpl[x] = a.Wp[x];
+  // layer-0 K order is c-major: step S covers field S%F, columns 16(S/F)..+15.
+  // Padding steps (S >= nS) multiply zero weights and skip the FM part.
+  for (int S = tid; S < 4 * nc0; S += 256) {
+    step_f[S] = S < nS ? S % F : -1;
+    step_col[S] = S < nS ? 16 * (S / F) : 0;
+  }
+
+  // chunk g -> LDS buffer b: TM lane-linear 1-KB DMAs per wave
+  auto dma = [&](int g, int b) {
+    const uint4* src = a.packed + (int64_t)g * CU + 64 * wv + l;
+    uint4* dst = wbuf0 + b * CU + 64 * wv;
+#pragma unroll
+    for (int q = 0; q < TM; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(src + 256 * q), (void*)(dst + 256 * q), 16,
+                                       0, 0);
+  };
+  // A fragment of tile t, k16 step s of a chunk: row 32t + r, unit 2s + h
+  const int swz = (r >> 1) & 7;
+  auto wfrag = [&](int b, int t, int s) {
+    return __builtin_bit_cast(bf16x8, wbuf0[b * CU + (32 * t + r) * 8 + ((2 * s + h) ^ swz)]);
+  };
+
+  // ---- layer-0 operand: gathered embeddings, one chunk ahead in registers ----
+  struct EChunk {
+    uint4 v[TBF ? 4 : 8];
+  };
+  const int myrow = 32 * wv + r;
+  auto eload = [&](EChunk& e, int c) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int S = 4 * c + s;
+      const int f = step_f[S];
+      const int64_t id = ids[myrow * F + (f >= 0 ? f : 0)];
+      const int col = step_col[S] + 8 * h;
+      if constexpr (TBF) {
+        e.v[s] = *reinterpret_cast<const uint4*>(
+            reinterpret_cast<const uint16_t*>(a.E) + id * k + col);
+      } else {
+        const uint4* p = reinterpret_cast<const uint4*>(
+            reinterpret_cast<const float*>(a.E) + id * k + col);
+        e.v[2 * s] = p[0];
+        e.v[2 * s + 1] = p[1];
+      }
+    }
+  };
+
+  f32x16 acc[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int x = 0; x < 16; ++x) acc[t][x] = 0.f;
+  float fs[8], fq[8];
+  float y2 = 0.f;
+
+  __syncthreads();   // ids, step tables visible
+  EChunk ea, eb;
+  eload(ea, 0);
+  dma(0, 0);
+  __syncthreads();   // vmcnt(0): chunk 0 in LDS
+
+  // Per K-chunk g (buffer g&1): DMA chunk g+1 into the other buffer (read in
+  // chunk g-1, released by its barrier), load the next embedding chunk into
+  // the other register set, run chunk g's MFMAs, then vmcnt(0) + barrier
+  // (__syncthreads) publishes chunk g+1.
+
+  // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
+  auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
+    const int b = c & 1;
+    if (c + 1 < nchunks) dma(c + 1, b ^ 1);
+    if (c + 1 < nc0) eload(en, c + 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int S = 4 * c + s;
+      float v[8];
+      uint4 bx;
+      if constexpr (TBF) {
+        bx = e.v[s];
+        const uint32_t x4[4] = {bx.x, bx.y, bx.z, bx.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[2 * j] = __uint_as_float(x4[j] << 16);
+          v[2 * j + 1] = __uint_as_float(x4[j] & 0xffff0000u);
+        }
+      } else {
+        const uint4 p = e.v[2 * s], q = e.v[2 * s + 1];
+        v[0] = __uint_as_float(p.x); v[1] = __uint_as_float(p.y);
+        v[2] = __uint_as_float(p.z); v[3] = __uint_as_float(p.w);
+        v[4] = __uint_as_float(q.x); v[5] = __uint_as_float(q.y);
+        v[6] = __uint_as_float(q.z); v[7] = __uint_as_float(q.w);
+        bx = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                        pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      }
+      const bf16x8 bb = __builtin_bit_cast(bf16x8, bx);
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(b, t, s), bb, acc[t], 0, 0, 0);
+      // FM second-order part over the same values (DFM.py:114-122)
+      const int f = step_f[S];
+      if (f == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { fs[j] = 0.f; fq[j] = 0.f; }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        fs[j] += v[j];
+        fq[j] += v[j] * v[j];
+      }
+      if (f == F - 1) {
+        const float* wc = wpl + F + step_col[S] + 8 * h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y2 += 0.5f * (fs[j] * fs[j] - fq[j]) * wc[j];
+      }
+    }
+    __syncthreads();
+  };
+  for (int c = 0; c < nc0; c += 2) {
+    chunk0(c, ea, eb);
+    if (c + 1 < nc0) chunk0(c + 1, eb, ea);
+  }
+
+  // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
+  uint32_t X[TM][8];
+  int g = nc0;
+  for (int i = 1; i < L; ++i) {
+    // epilogue of layer i-1: bias + ReLU (DFM.py:127-128, every layer), bf16,
+    // then into B-operand order (k = 8*half + j) with one swap per pair
+    const float* bli = blv + (i - 1) * NR;
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+      float v[16];
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const int n = 32 * t + 8 * (x >> 2) + 4 * h + (x & 3);
+        v[x] = fmaxf(acc[t][x] + bli[n], 0.f);
+        acc[t][x] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) X[t][q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+      swap_halves(X[t][0], X[t][2]);
+      swap_halves(X[t][1], X[t][3]);
+      swap_halves(X[t][4], X[t][6]);
+      swap_halves(X[t][5], X[t][7]);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c, ++g) {
+      const int b = g & 1;
+      if (g + 1 < nchunks) dma(g + 1, b ^ 1);
+#pragma unroll
+      for (int ts = 0; ts < 2; ++ts) {
+        const int tin = 2 * c + ts;
+        if (tin < TM) {
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const uint4 bx = make_uint4(X[tin][4 * s], X[tin][4 * s + 1], X[tin][4 * s + 2],
+                                        X[tin][4 * s + 3]);
+            const bf16x8 bb = __builtin_bit_cast(bf16x8, bx);
+#pragma unroll
+            for (int t = 0; t < TM; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(b, t, 2 * ts + s), bb,
+                                                               acc[t], 0, 0, 0);
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- last layer: relu(acc + b) · Wp_deep, FM part, bias terms ----
+  const float* blL = blv + (L - 1) * NR;
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      const int n = 32 * t + 8 * (x >> 2) + 4 * h + (x & 3);
+      part += fmaxf(acc[t][x] + blL[n], 0.f) * vl[n];
+    }
+  part += __shfl_xor(part, 32, kWave);
+  y2 += __shfl_xor(y2, 32, kWave);
+  const int64_t m = m0 + myrow;
+  if (h == 0 && m < a.B) {
+    float y1 = 0.f;
+    for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
+    a.out[m] = ((y1 + y2) + a.bp) + part;
+  }
+}
+
+static int fused_tm(int maxT) {
+  const int tms[] = {2, 4, 5, 7, 8, 10, 13};
+  for (int t : tms)
+    if (maxT <= t) return t;
+  return 0;
+}
+
+static int fused_max_tiles(int L, const int32_t* dims) {
+  int maxT = 0;
+  for (int i = 0; i < L; ++i) {
+    const int T = (dims[i] + 31) / 32;
+    maxT = T > maxT ? T : maxT;
+  }
+  return maxT;
+}
+
+bool dfm_fused_eligible(int L, const int32_t* dims) {
+  return L >= 1 && L <= kFusedMaxLayers && fused_tm(fused_max_tiles(L, dims)) > 0;
+}
+
+// workspace for the packed weights; an upper bound over F·k <= 16·512 so the
+// size is known from (nlayers, dims) alone
+size_t dfm_fused_pack_bytes(int L, const int32_t* dims) {
+  const int TM = fused_tm(fused_max_tiles(L, dims));
+  const int nc0 = (kFusedMaxF * kFusedMaxK / 16 + 3) / 4;
+  return (size_t)(nc0 + (L - 1) * ((TM + 1) / 2)) * 32 * TM * 8 * 16;
+}
+
+// returns false when the shape is outside the fused kernel's envelope
+bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
+                      bool tbf, const float* w, int L, const int32_t* dims,
+                      const void* const* Wt, const float* const* bias, const float* Wp, float bp,
+                      float* out, void* pack_ws, hipStream_t st) {
+  if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k % 16 || k > kFusedMaxK) return false;
+  for (int i = 0; i < L; ++i)
+    if (reinterpret_cast<uintptr_t>(Wt[i]) & 15) return false;
+  const int TM = fused_tm(fused_max_tiles(L, dims));
+  FusedDfmArgs a{};
+  a.idx = idx; a.B = B; a.F = F; a.k = k; a.E = E; a.M = M; a.w = w; a.L = L;
+  int kin = F * k;
+  for (int i = 0; i < L; ++i) {
+    a.dims[i] = dims[i];
+    a.ldb[i] = (kin + 7) & ~7;
+    a.Wt[i] = reinterpret_cast<const uint16_t*>(Wt[i]);
+    a.bias[i] = bias[i];
+    kin = dims[i];
+  }
+  a.Wp = Wp; a.bp = bp; a.out = out;
+  a.packed = reinterpret_cast<const uint4*>(pack_ws);
+  const int nS = F * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;
+  const int64_t units = (int64_t)(nc0 + (L - 1) * NC) * 32 * TM * 8;
+  const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+  hipLaunchKernelGGL(dfm_pack_weights, dim3(pblocks), dim3(256), 0, st, a, TM, nc0, NC,
+                     reinterpret_cast<uint4*>(pack_ws));
+  const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
+#define HHFM_FUSED(T)                                                                    \
+  case T:                                                                                \
+    if (tbf) hipLaunchKernelGGL((dfm_fused<true, T>), grid, dim3(256), 0, st, a);        \
+    else hipLaunchKernelGGL((dfm_fused<false, T>), grid, dim3(256), 0, st, a);           \
+    break;
+  switch (TM) {
+    HHFM_FUSED(2)
+    HHFM_FUSED(4)
+    HHFM_FUSED(5)
+    HHFM_FUSED(7)
+    HHFM_FUSED(8)
+    HHFM_FUSED(10)
+    HHFM_FUSED(13)
+    default: return false;
+  }
+#undef HHFM_FUSED
+  return true;
+}
+
+}  // namespace hhfm

@@ -18,9 +18,18 @@
 // Epilogues: (a) relu(acc + bias) stored as bf16 / f32 (DFM.py:127-128);
 // (b) relu(acc + bias) · v summed over the tile's columns into per-row
 // partials (last hidden layer fused with the concat projection, DFM.py:137).
+#include <cstdlib>
+
 #include "gemm_mfma.h"
 
 namespace hhfm {
+
+bool dfm_fused_eligible(int L, const int32_t* dims);
+size_t dfm_fused_pack_bytes(int L, const int32_t* dims);
+bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
+                      bool tbf, const float* w, int L, const int32_t* dims,
+                      const void* const* Wt, const float* const* bias, const float* Wp, float bp,
+                      float* out, void* pack_ws, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // FM part of DeepFM and the final reduce
@@ -97,9 +106,10 @@ static void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds,
                        K, base, os, oi);
 }
 
-// workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL]
+// workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL][packed weights of
+// the fused bf16 kernel, when its envelope admits the layer widths]
 struct DfmPlan {
-  size_t off_base, off_part, off_h0, off_h1, total;
+  size_t off_base, off_part, off_h0, off_h1, off_pack, total;
   int maxL, ntl;
 };
 
@@ -118,6 +128,9 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   p.off_part = off; off += al256((size_t)B * p.ntl * 4);
   p.off_h0 = off; off += al256((size_t)B * p.maxL * esz);
   p.off_h1 = off; off += al256((size_t)B * p.maxL * esz);
+  p.off_pack = off;
+  if (mlp_dtype == HHFM_BF16 && dfm_fused_eligible(nlayers, dims))
+    off += al256(dfm_fused_pack_bytes(nlayers, dims));
   p.total = off;
   return p;
 }
@@ -141,6 +154,17 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
                             float bp, float* out, char* ws, const DfmPlan& p, hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
+  // bf16 MLP: one fused kernel per 128-row block when the shape fits
+  // (dfm_fused.hip); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
+  static const bool layered = [] {
+    const char* e = getenv("HHFM_DFM_LAYERED");
+    return e && e[0] == '1';
+  }();
+  if (bf && !layered &&
+      p.total > p.off_pack &&
+      dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, w, nlayers, dims, Wt, bias, Wp,
+                       bp, out, ws + p.off_pack, st))
+    return (int)hipGetLastError();
   float* base = reinterpret_cast<float*>(ws + p.off_base);
   float* part = reinterpret_cast<float*>(ws + p.off_part);
   void* h[2] = {ws + p.off_h0, ws + p.off_h1};

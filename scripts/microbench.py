@@ -94,9 +94,14 @@ if not only or "dfm" in only:
         off += c
     X = torch.stack(cols, 1).to(torch.int32).contiguous()
     flops_row = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
-    for mdt, name in ((torch.bfloat16, "dfm_c5_bf16"), (torch.float32, "dfm_c5_f32")):
+    legs = [(torch.bfloat16, torch.float32, "dfm_c5_bf16"),
+            (torch.bfloat16, torch.bfloat16, "dfm_c5_bf16_tbf16"),
+            (torch.float32, torch.float32, "dfm_c5_f32")]
+    if os.environ.get("MB_DFM_LEGS"):
+        legs = [x for x in legs if x[2] in os.environ["MB_DFM_LEGS"].split(",")]
+    for mdt, tdt, name in legs:
         m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
-                   mlp_dtype=mdt)
+                   mlp_dtype=mdt, table_dtype=tdt)
         m.validate = False
         Wt, bs, dims, Wp, bp = m._prepared()
         out = torch.empty(B, device=dev)

@@ -144,3 +144,33 @@ def test_topk_dense_matches_sort():
         rs, ri = orc.top_k(S, K)
         assert np.array_equal(i.cpu().numpy(), ri + 5)
         assert np.array_equal(s.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("F,k,layers,tdt,B", [
+    (5, 16, [33], "bf16", 129),                 # fused, 1 layer, bf16 table, ragged tail
+    (3, 48, [64, 96, 33, 20], "f32", 1000),     # fused, 4 layers, odd widths
+    (11, 32, [128, 416], "bf16", 1),            # fused, widest envelope (13 tiles), one row
+    (5, 64, [450, 64], "f32", 300),             # layered fallback: 15 tiles
+    (5, 64, [64, 64, 64, 64, 64], "f32", 257),  # layered fallback: 5 layers
+    (5, 40, [100], "f32", 77),                  # layered fallback: k % 16 != 0
+])
+def test_dfm_bf16_envelope(F, k, layers, tdt, B):
+    """bf16 MLP: the fused per-row-block kernel (dfm_fused.hip) and the
+    layer-by-layer GEMM path, both against the bf16-rounding oracle."""
+    rng = np.random.default_rng(F * 1000 + k)
+    M = 997
+    tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
+    m = _model((100, 200, M, F, k, layers), mlp_dtype=torch.bfloat16, table_dtype=tdtype)
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    W = m.get_weights()
+    L = len(layers)
+    Ls = [W[f"layer_{i}"] for i in range(L)]
+    Bs = [W[f"bias_{i}"] for i in range(L)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    if tdt == "bf16":
+        E = bf16_round(E)
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    got = m.score_rows(X)[:, 0]
+    ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
