@@ -207,53 +207,74 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   // (__syncthreads) publishes chunk g+1.
 
   // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
+  // One 64-deep chunk from LDS buffer b: the TM weight fragments of step
+  // j+1 are read right behind step j's MFMAs (software pipelined; one wave
+  // per SIMD has no other wave to hide LDS latency), bop(j) supplies the B
+  // operand of step j and side(j) runs beside it.
+  auto run_chunk = [&](int b, auto&& bop, auto&& side) {
+    bf16x8 fa[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) fa[t] = wfrag(b, t, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16x8 bb = bop(j);
+#pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t], bb, acc[t], 0, 0, 0);
+        if (j < 3) fa[t] = wfrag(b, t, j + 1);
+        __builtin_amdgcn_sched_barrier(0);   // keep the read right behind its MFMA
+      }
+      side(j);
+    }
+  };
+
+  // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
   auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
     const int b = c & 1;
     if (c + 1 < nchunks) dma(c + 1, b ^ 1);
     if (c + 1 < nc0) eload(en, c + 1);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int S = 4 * c + s;
-      float v[8];
+    float v[4][8];
+    auto bop = [&](int j) {
       uint4 bx;
       if constexpr (TBF) {
-        bx = e.v[s];
+        bx = e.v[j];
         const uint32_t x4[4] = {bx.x, bx.y, bx.z, bx.w};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[2 * j] = __uint_as_float(x4[j] << 16);
-          v[2 * j + 1] = __uint_as_float(x4[j] & 0xffff0000u);
+        for (int q = 0; q < 4; ++q) {
+          v[j][2 * q] = __uint_as_float(x4[q] << 16);
+          v[j][2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
         }
       } else {
-        const uint4 p = e.v[2 * s], q = e.v[2 * s + 1];
-        v[0] = __uint_as_float(p.x); v[1] = __uint_as_float(p.y);
-        v[2] = __uint_as_float(p.z); v[3] = __uint_as_float(p.w);
-        v[4] = __uint_as_float(q.x); v[5] = __uint_as_float(q.y);
-        v[6] = __uint_as_float(q.z); v[7] = __uint_as_float(q.w);
-        bx = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
-                        pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+        const uint4 p = e.v[2 * j], q = e.v[2 * j + 1];
+        v[j][0] = __uint_as_float(p.x); v[j][1] = __uint_as_float(p.y);
+        v[j][2] = __uint_as_float(p.z); v[j][3] = __uint_as_float(p.w);
+        v[j][4] = __uint_as_float(q.x); v[j][5] = __uint_as_float(q.y);
+        v[j][6] = __uint_as_float(q.z); v[j][7] = __uint_as_float(q.w);
+        bx = make_uint4(pack_bf16x2(v[j][0], v[j][1]), pack_bf16x2(v[j][2], v[j][3]),
+                        pack_bf16x2(v[j][4], v[j][5]), pack_bf16x2(v[j][6], v[j][7]));
       }
-      const bf16x8 bb = __builtin_bit_cast(bf16x8, bx);
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(b, t, s), bb, acc[t], 0, 0, 0);
-      // FM second-order part over the same values (DFM.py:114-122)
+      return __builtin_bit_cast(bf16x8, bx);
+    };
+    // FM second-order part over the same values (DFM.py:114-122)
+    auto side = [&](int j) {
+      const int S = 4 * c + j;
       const int f = step_f[S];
       if (f == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { fs[j] = 0.f; fq[j] = 0.f; }
+        for (int q = 0; q < 8; ++q) { fs[q] = 0.f; fq[q] = 0.f; }
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        fs[j] += v[j];
-        fq[j] += v[j] * v[j];
+      for (int q = 0; q < 8; ++q) {
+        fs[q] += v[j][q];
+        fq[q] += v[j][q] * v[j][q];
       }
       if (f == F - 1) {
         const float* wc = wpl + F + step_col[S] + 8 * h;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) y2 += 0.5f * (fs[j] * fs[j] - fq[j]) * wc[j];
+        for (int q = 0; q < 8; ++q) y2 += 0.5f * (fs[q] * fs[q] - fq[q]) * wc[q];
       }
-    }
+    };
+    run_chunk(b, bop, side);
     __syncthreads();
   };
   for (int c = 0; c < nc0; c += 2) {
@@ -288,22 +309,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     for (int c = 0; c < NC; ++c, ++g) {
       const int b = g & 1;
       if (g + 1 < nchunks) dma(g + 1, b ^ 1);
-#pragma unroll
-      for (int ts = 0; ts < 2; ++ts) {
-        const int tin = 2 * c + ts;
-        if (tin < TM) {
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const uint4 bx = make_uint4(X[tin][4 * s], X[tin][4 * s + 1], X[tin][4 * s + 2],
-                                        X[tin][4 * s + 3]);
-            const bf16x8 bb = __builtin_bit_cast(bf16x8, bx);
-#pragma unroll
-            for (int t = 0; t < TM; ++t)
-              acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfrag(b, t, 2 * ts + s), bb,
-                                                               acc[t], 0, 0, 0);
-          }
-        }
-      }
+      auto bop = [&](int j) {   // step j = input tile 2c + j/2, k16 half j%2
+        const int tin = 2 * c + (j >> 1), s2 = 4 * (j & 1);
+        const uint4 bx = tin < TM ? make_uint4(X[tin][s2], X[tin][s2 + 1], X[tin][s2 + 2],
+                                               X[tin][s2 + 3])
+                                  : make_uint4(0, 0, 0, 0);
+        return __builtin_bit_cast(bf16x8, bx);
+      };
+      run_chunk(b, bop, [](int) {});
       __syncthreads();
     }
   }
