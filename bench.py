@@ -314,11 +314,18 @@ def main():
     del idx, E, w, out
     torch.cuda.empty_cache()
     extra = {}
+    # the extra legs never cost the headline line: a failure is recorded, not raised
     if "catalog" in legs:
-        extra["catalog_c4"] = catalog_leg(dev, world, rank)
+        try:
+            extra["catalog_c4"] = catalog_leg(dev, world, rank)
+        except Exception as e:  # noqa: BLE001
+            extra["catalog_c4"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
     if "hr" in legs and rank == 0:
-        extra["hr_at_10"] = hr_leg(dev, args.hr_epochs)
+        try:
+            extra["hr_at_10"] = hr_leg(dev, args.hr_epochs)
+        except Exception as e:  # noqa: BLE001
+            extra["hr_at_10"] = {"error": f"{type(e).__name__}: {e}"}
     if extra:
         result["extra"] = extra
     if rank == 0:
