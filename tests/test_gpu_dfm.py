@@ -109,29 +109,38 @@ def test_dfm_forward_shapes(mlp, k, layers):
         assert np.all(np.abs(got - ref) <= 5e-3 * mag)
 
 
-def test_dfm_catalog_topk_chunked():
-    """Query chunking (chunk_rows < B*N) gives the same top-K as one pass."""
+@pytest.mark.parametrize("mlp", ["f32", "bf16"])
+def test_dfm_catalog_topk_chunked(mlp):
+    """Query chunking (chunk_rows < B*N) gives the same top-K as one pass
+    (bf16: the fused kernel scores the chunks; oracle rounds like it)."""
     from hhfm_amd import ops
     rng = np.random.default_rng(8)
     nu, ni, F, k = 50, 700, 5, 32
     M = nu + ni + 12
-    m = _model((nu, ni, M, F, k, [64, 48]))
+    mdt = torch.float32 if mlp == "f32" else torch.bfloat16
+    m = _model((nu, ni, M, F, k, [64, 48]), mlp_dtype=mdt)
     A = np.stack([rng.integers(0, nu, 37), rng.integers(nu, nu + ni, 37),
                   rng.integers(nu + ni, nu + ni + 7, 37), rng.integers(nu + ni + 7, nu + ni + 9, 37),
                   rng.integers(nu + ni + 9, M, 37)], 1).astype(np.int32)
     W = m.get_weights()
     Ls = [W["layer_0"], W["layer_1"]]
     Bs = [W["bias_0"], W["bias_1"]]
-    sc = orc.dfm_catalog_scores(A, W["feature_embeddings"], W["feature_bias"][:, 0], Ls, Bs,
-                                W["concat_projection"], float(W["concat_bias"]), nu, ni)
+    if mlp == "f32":
+        sc = orc.dfm_catalog_scores(A, W["feature_embeddings"], W["feature_bias"][:, 0], Ls, Bs,
+                                    W["concat_projection"], float(W["concat_bias"]), nu, ni)
+    else:
+        rows = np.repeat(A, ni, 0)
+        rows[:, 1] = np.tile(np.arange(nu, nu + ni), len(A))
+        sc = _bf16_oracle(rows, W["feature_embeddings"], W["feature_bias"][:, 0], Ls, Bs,
+                          W["concat_projection"], float(W["concat_bias"])).reshape(len(A), ni)
     Wt, bs, dims, Wp, bp = m._prepared()
     q = torch.from_numpy(A).cuda()
     for chunk in (1 << 20, 1000, 701):
         s, i = ops.dfm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,
                                     dims, Wp, bp, 1, nu, ni, 20, 0, chunk)
         rs, ri = orc.top_k(sc, 21)
-        mism, amb = orc.topk_index_agreement(rs, ri[:, :20], i.cpu().numpy(),
-                                             1e-5 * np.abs(sc).max(1, keepdims=True))
+        tol = (1e-5 if mlp == "f32" else 5e-3) * np.abs(sc).max(1, keepdims=True)
+        mism, amb = orc.topk_index_agreement(rs, ri[:, :20], i.cpu().numpy(), tol)
         assert mism == 0, (chunk, mism, amb)
 
 
