@@ -69,9 +69,148 @@ __global__ __launch_bounds__(256) void afm_rows_finish(
   }
 }
 
+// ---- A1 fused: one wave scores floor(32/np) rows per step --------------------
+// Every (row, pair) "combo" of R = floor(32/np) rows is one MFMA column: the
+// attention pre-activations are computed TRANSPOSED, D[unit][combo] =
+// Σ_k Wᵀ[unit][k]·(e_i⊙e_j)[combo][k], with v_mfma_f32_32x32x2_f32 (exact
+// fp32 products, fp32 accumulation): A = Wᵀ rows from an XOR-swizzled LDS
+// image, B = the combo's pair product formed in registers from two 16-B
+// gathers per 8 k.  A lane then holds one combo and 16 attention units per
+// tile, so relu(·+b)·p sums in-lane; the same products dotted with P give
+// s = (e_i⊙e_j)·P, and out = Σ_p softmax(logit)_p·s_p + Σw + w0 — the
+// AFM.py:118-142 value with Σ_p att_p Σ_c(...) re-associated per pair.  Pair
+// products, logits and attention weights never leave registers.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kAfmMaxK = 256;
+constexpr int kAfmFusedMaxF = 8;     // F(F-1)/2 <= 28 combos of one row fit 32 columns
+constexpr int kAfmFusedImg = 32 * 512;   // floats: NT*32 units x k <= 512*32
+
+template <bool TBF, int NT>
+__global__ __launch_bounds__(256) void afm_rows_fused(
+    const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
+    int k, const float* __restrict__ w, float w0, const float* __restrict__ Wt,
+    const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
+    const float* __restrict__ P, float* __restrict__ out) {
+  constexpr int NA = NT * 32;
+  __shared__ __attribute__((aligned(16))) float smem[kAfmFusedImg + kAfmMaxK + 2 * NA];
+  float4* img = reinterpret_cast<float4*>(smem);
+  float* Pl = smem + kAfmFusedImg;
+  float* bl = Pl + kAfmMaxK;
+  float* apl = bl + NA;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int j = l & 31, h = l >> 5;
+  const int U = k / 4;                       // 16-B units per Wᵀ row
+  int sw = 1;                                // XOR group: largest power of 2 dividing U, <= 16
+  while (sw < 16 && U % (2 * sw) == 0) sw *= 2;
+  const int SW = sw - 1;
+  for (int x = tid; x < NA * U; x += 256) {
+    const int u = x / U, c = x - u * U;
+    const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    img[u * U + (c ^ (u & SW))] = v;
+  }
+  for (int x = tid; x < k; x += 256) Pl[x] = P[x];
+  for (int x = tid; x < NA; x += 256) {
+    bl[x] = x < A ? att_b[x] : 0.f;
+    apl[x] = x < A ? att_p[x] : 0.f;
+  }
+  __syncthreads();
+
+  const int np = F * (F - 1) / 2, R = 32 / np;
+  const int r = j / np, p = j - r * np;
+  int pi, pj;
+  pair_ij(p, F, pi, pj);                     // (only read when this lane's combo is live)
+  const bool live = r < R;
+  const int64_t nblk = (B + R - 1) / R;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += wstride) {
+    const int64_t row = blk * R + r;
+    const bool ok = live && row < B;
+    const int64_t rr = ok ? row : 0;
+    const int64_t ia = clamp_id(idx[rr * F + (live ? pi : 0)], M);
+    const int64_t ib = clamp_id(idx[rr * F + (live ? pj : 1)], M);
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) acc[n][x] = 0.f;
+    float sP = 0.f;
+    // this lane's 4 k of 8-k step t, one step of gathers in flight ahead
+    auto gather = [&](int t, float4& x, float4& y) {
+      const int c0 = 8 * t + 4 * h;
+      if constexpr (TBF) {
+        const uint2 u = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const uint16_t*>(E) + ia * k + c0);
+        const uint2 v = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const uint16_t*>(E) + ib * k + c0);
+        x = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+        y = make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                        __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+      } else {
+        x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ia * k + c0);
+        y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ib * k + c0);
+      }
+    };
+    // Σw of the row: lanes p < F of the row's group fetch one field each
+    const float wf = (ok && p < F) ? w[clamp_id(idx[row * F + p], M)] : 0.f;
+    float4 xa, ya;
+    gather(0, xa, ya);
+    const int KQ = k / 8;
+    for (int t = 0; t < KQ; ++t) {
+      float4 xn = xa, yn = ya;
+      if (t + 1 < KQ) gather(t + 1, xn, yn);
+      const int c0 = 8 * t + 4 * h;
+      const float ea[4] = {xa.x, xa.y, xa.z, xa.w}, eb[4] = {ya.x, ya.y, ya.z, ya.w};
+      float pe[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pe[e] = ea[e] * eb[e];
+        sP = fmaf(pe[e], Pl[c0 + e], sP);
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int u = 32 * n + j;            // A-operand row = attention unit
+        const float4 wa = img[u * U + ((2 * t + h) ^ (u & SW))];
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, pe[0], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, pe[1], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, pe[2], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, pe[3], acc[n], 0, 0, 0);
+      }
+      xa = xn;
+      ya = yn;
+    }
+    // logit of this lane's combo: Σ_units p·relu(acc + b)  (AFM.py:112-117)
+    float lg = 0.f;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const int u = 32 * n + 8 * (x >> 2) + 4 * h + (x & 3);
+        lg = fmaf(fmaxf(acc[n][x] + bl[u], 0.f), apl[u], lg);
+      }
+    lg += __shfl_xor(lg, 32, kWave);
+    sP += __shfl_xor(sP, 32, kWave);
+    // softmax over the row's np pairs (tf.nn.softmax, AFM.py:125) and the
+    // attention-weighted sum of the pair scores
+    const int base = (live ? r : 0) * np;
+    float mx = kNegInf;
+    for (int q = 0; q < np; ++q) mx = fmaxf(mx, __shfl(lg, base + q, kWave));
+    float se = 0.f, num = 0.f;
+    for (int q = 0; q < np; ++q) {
+      const float ee = expf(__shfl(lg, base + q, kWave) - mx);
+      se += ee;
+      num = fmaf(ee, __shfl(sP, base + q, kWave), num);
+    }
+    float fb = 0.f;
+    for (int f = 0; f < F; ++f) fb += __shfl(wf, base + f, kWave);
+    if (ok && p == 0 && h == 0) out[row] = (num / se + fb) + w0;   // add_n, AFM.py:142
+  }
+}
+
 // ---- A2 prep: one 64-thread block per query ------------------------------------
 // uf = [E[q0], E[q2], ..., E[q_{F-1}]] (u_f = F-1 fields, AFM.py:210-212)
-constexpr int kAfmMaxK = 256, kAfmMaxUF = 15;
+constexpr int kAfmMaxUF = 15;
 
 __global__ __launch_bounds__(64) void afm_cat_prep(
     const int32_t* __restrict__ q, int64_t B, int F, const void* __restrict__ E, int t_bf16,
@@ -222,6 +361,29 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
   if (!workspace || ws_bytes < need) return HHFM_EWORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int np = F * (F - 1) / 2;
+  {  // fused path: F <= 8, k % 8 == 0, A <= 128, (A padded to 32) x k <= 32 x 512
+    const int NT = (A + 31) / 32;
+    if (F <= kAfmFusedMaxF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 && NT * k <= 512) {
+      const int R = 32 / np;
+      const int64_t nblk = (B + R - 1) / R;
+      int64_t blocks = (nblk + 3) / 4;
+      if (blocks > 2048) blocks = 2048;
+      const bool tb = dtype == HHFM_BF16;
+#define HHFM_AFM_FUSED(N)                                                                   \
+  if (NT == N) {                                                                           \
+    if (tb) hipLaunchKernelGGL((afm_rows_fused<true, N>), dim3((unsigned)blocks), dim3(256), 0, st, \
+                               idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
+    else hipLaunchKernelGGL((afm_rows_fused<false, N>), dim3((unsigned)blocks), dim3(256), 0, st, \
+                            idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);   \
+    return (int)hipGetLastError();                                                         \
+  }
+      HHFM_AFM_FUSED(1)
+      HHFM_AFM_FUSED(2)
+      HHFM_AFM_FUSED(3)
+      HHFM_AFM_FUSED(4)
+#undef HHFM_AFM_FUSED
+    }
+  }
   const int ntl = (A + GBN - 1) / GBN;
   float* part = reinterpret_cast<float*>(workspace);
   GemmArgs g{};
