@@ -21,15 +21,39 @@ HHFM_DEV int lane_id() { return threadIdx.x & (kWave - 1); }
 HHFM_DEV float shfl_f(float v, int src) { return __shfl(v, src, kWave); }
 HHFM_DEV int32_t shfl_i(int32_t v, int src) { return __shfl(v, src, kWave); }
 
+// v from lane (self ^ d), d a power of two < 64, without the LDS crossbar
+// where a DPP pattern exists (ds_bpermute costs an LDS round trip per step):
+//   d = 1, 2: quad_perm; d = 4: row_shl/row_shr 4 + lane select; d = 8:
+//   row_ror 8; d = 16: ds_swizzle xor mode (no address VGPR); d = 32:
+//   v_permlane32_swap.
+HHFM_DEV int32_t xor_lane(int32_t v, int d) {
+  switch (d) {
+    case 1: return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);   // [1,0,3,2]
+    case 2: return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);   // [2,3,0,1]
+    case 4: {
+      const int32_t up = __builtin_amdgcn_update_dpp(v, v, 0x104, 0xF, 0xF, false);  // row_shl:4
+      const int32_t dn = __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+      return (lane_id() & 4) ? dn : up;
+    }
+    case 8: return __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: return __builtin_amdgcn_ds_swizzle(v, 0x401F);                    // xor 16 in 32
+    default: {   // 32: swap(a=v, b=v) leaves a = [v_lo | v_lo], b = [v_hi | v_hi]
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      return (int32_t)(lane_id() < 32 ? r[1] : r[0]);
+    }
+  }
+}
+HHFM_DEV float xor_lane(float v, int d) {
+  return __int_as_float(xor_lane(__float_as_int(v), d));
+}
+
 // One compare-exchange step of a bitonic network: keep the better of
 // (self, lane^d) when keep_better, else the worse.
 HHFM_DEV void cx(float& s, int32_t& i, int d, bool keep_better) {
-  const int l = lane_id();
-  const float ps = __shfl_xor(s, d, kWave);
-  const int32_t pi = __shfl_xor(i, d, kWave);
+  const float ps = xor_lane(s, d);
+  const int32_t pi = xor_lane(i, d);
   const bool pb = better(ps, pi, s, i);
   const bool take = keep_better ? pb : !pb;
-  (void)l;
   s = take ? ps : s;
   i = take ? pi : i;
 }
