@@ -341,6 +341,238 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 MLP (the reference numerics): v_mfma_f32_16x16x4_f32 (exact fp32
+// products, fp32 accumulation), 4 waves x 16 rows per workgroup (16-row
+// tiles: 32x32 ones would need 208 accumulator + 208 activation registers
+// per lane at 416 units, beyond one wave's 512).  Each lane group kq = lane/16 supplies
+// 4 consecutive k of every 16-k step (one 16-B gather / weight unit feeds 4
+// MFMAs), and a 16x16 result tile holds, per lane group q, units 4q..4q+3 —
+// exactly the k a lane group supplies in the next layer, so a layer's fp32
+// output IS the next layer's B operand in registers, no reordering.  Chunks
+// are 32 k deep; layer 0 runs its 16-column blocks field-minor (c-major).
+// ---------------------------------------------------------------------------
+constexpr int kF32Waves = 4;
+constexpr int kF32Rows = kF32Waves * 16;   // rows per workgroup
+
+__global__ __launch_bounds__(256) void dfm_pack_weights_f32(FusedDfmArgs a, int TM, int nc0,
+                                                            uint4* __restrict__ out) {
+  const int NR = 32 * TM;
+  const int nB = a.F * (a.k / 16);            // layer-0 16-column blocks
+  const int64_t total = (int64_t)(nc0 + (a.L - 1) * TM) * NR * 8;
+  const float* const* Wf = reinterpret_cast<const float* const*>(a.Wt);
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(x / (NR * 8));
+    const int rem = (int)(x - (int64_t)g * NR * 8);
+    const int n = rem >> 3, u = (rem & 7) ^ ((n >> 1) & 7);
+    int i, kk;
+    bool ok;
+    if (g < nc0) {   // chunk = 2 blocks of 16 columns, unit u = (block u/4, quarter u%4)
+      i = 0;
+      const int b = 2 * g + (u >> 2);
+      ok = b < nB;
+      kk = (b % a.F) * a.k + 16 * (b / a.F) + 4 * (u & 3);
+    } else {
+      i = 1 + (g - nc0) / TM;
+      kk = 32 * ((g - nc0) % TM) + 4 * u;
+      ok = kk < a.ldb[i];
+    }
+    ok = ok && n < a.dims[i];
+    out[x] = ok ? *reinterpret_cast<const uint4*>(Wf[i] + (int64_t)n * a.ldb[i] + kk)
+                : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <bool TBF, int TM>
+__global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
+  constexpr int NR = TM * 32;
+  constexpr int T16 = 2 * TM;                // 16-unit output tiles
+  constexpr int CU = NR * 8;
+  constexpr int kMaxBlocks = kFusedMaxF * kFusedMaxK / 16 + 2;
+  constexpr int kW = 2 * CU * 16;
+  constexpr int kIds = kW, kBl = kIds + kF32Rows * kFusedMaxF * 4;
+  constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
+  constexpr int kSf = kWp + (kFusedMaxF + kFusedMaxK) * 4, kSc = kSf + kMaxBlocks * 4;
+  constexpr int kSmem = kSc + kMaxBlocks * 4;
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];   // ONE LDS object
+  uint4* wbuf0 = reinterpret_cast<uint4*>(smem);
+  int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
+  float* blv = reinterpret_cast<float*>(smem + kBl);
+  float* vl = reinterpret_cast<float*>(smem + kVl);
+  float* wpl = reinterpret_cast<float*>(smem + kWp);
+  int32_t* blk_f = reinterpret_cast<int32_t*>(smem + kSf);
+  int32_t* blk_col = reinterpret_cast<int32_t*>(smem + kSc);
+
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int r = l & 15, kq = l >> 4;         // row in the wave's 16 / k quarter
+  const int64_t m0 = (int64_t)blockIdx.x * kF32Rows;
+  const int F = a.F, k = a.k, L = a.L;
+  const int nB = F * (k / 16);
+  const int nc0 = (nB + 1) / 2;
+  const int nchunks = nc0 + (L - 1) * TM;
+
+  for (int x = tid; x < kF32Rows * F; x += 256) {
+    const int64_t m = m0 + x / F;
+    ids[x] = m < a.B ? clamp_id(a.idx[m * F + x % F], a.M) : 0;
+  }
+  for (int i = 0; i < L; ++i)
+    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
+  for (int x = tid; x < F + k; x += 256) wpl[x] = a.Wp[x];
+  for (int b = tid; b < 2 * nc0; b += 256) {
+    blk_f[b] = b < nB ? b % F : -1;
+    blk_col[b] = b < nB ? 16 * (b / F) : 0;
+  }
+
+  // chunk g -> buffer b: CU/64 lane-linear 1-KB DMAs spread over 8 waves
+  auto dma = [&](int g, int b) {
+    const uint4* src = a.packed + (int64_t)g * CU;
+    uint4* dst = wbuf0 + b * CU;
+#pragma unroll
+    for (int q = 0; q < (TM * 4 + kF32Waves - 1) / kF32Waves; ++q) {
+      const int ins = wv + kF32Waves * q;      // 1-KB piece (TM*4 of them)
+      if (ins < TM * 4)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 64 * ins + l),
+                                         (void*)(dst + 64 * ins), 16, 0, 0);
+    }
+  };
+  // A fragment: output unit 16*t + r, 16-B weight unit u of the chunk
+  auto wfrag = [&](int b, int t, int u) {
+    const int row = 16 * t + r;
+    return __builtin_bit_cast(float4, wbuf0[b * CU + row * 8 + (u ^ ((row >> 1) & 7))]);
+  };
+
+  struct EChunk {
+    float4 v[2];
+  };
+  const int myrow = 16 * wv + r;
+  auto eload = [&](EChunk& e, int c) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int b = 2 * c + q;
+      const int f = blk_f[b];
+      const int64_t id = ids[myrow * F + (f >= 0 ? f : 0)];
+      const int col = blk_col[b] + 4 * kq;
+      if constexpr (TBF) {
+        const uint2 x = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const uint16_t*>(a.E) + id * k + col);
+        e.v[q] = make_float4(__uint_as_float(x.x << 16), __uint_as_float(x.x & 0xffff0000u),
+                             __uint_as_float(x.y << 16), __uint_as_float(x.y & 0xffff0000u));
+      } else {
+        e.v[q] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.E) + id * k +
+                                                  col);
+      }
+    }
+  };
+
+  f32x4 acc[T16];
+#pragma unroll
+  for (int t = 0; t < T16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float fs[4], fq[4];
+  float y2 = 0.f;
+
+  __syncthreads();
+  EChunk ea, eb;
+  eload(ea, 0);
+  dma(0, 0);
+  __syncthreads();
+
+  // one 16-k step (weight units 4s..4s+3 of the chunk; lane group kq takes
+  // unit 4s+kq): 4 MFMAs per output tile, next tile's fragment read ahead
+  auto step = [&](int b, int s, const float (&bv)[4]) {
+    float4 fa = wfrag(b, 0, 4 * s + kq);
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+      const float4 cur = fa;
+      if (t + 1 < T16) fa = wfrag(b, t + 1, 4 * s + kq);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.x, bv[0], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.y, bv[1], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.z, bv[2], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.w, bv[3], acc[t], 0, 0, 0);
+    }
+  };
+
+  // ----- layer 0 -----
+  auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
+    const int b = c & 1;
+    if (c + 1 < nchunks) dma(c + 1, b ^ 1);
+    if (c + 1 < nc0) eload(en, c + 1);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const float bv[4] = {e.v[q].x, e.v[q].y, e.v[q].z, e.v[q].w};
+      step(b, q, bv);
+      // FM second-order part (DFM.py:114-122) over the same fp32 values
+      const int B = 2 * c + q;
+      const int f = blk_f[B];
+      if (f == 0) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) { fs[x] = 0.f; fq[x] = 0.f; }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        fs[x] += bv[x];
+        fq[x] += bv[x] * bv[x];
+      }
+      if (f == F - 1) {
+        const float* wc = wpl + F + blk_col[B] + 4 * kq;
+#pragma unroll
+        for (int x = 0; x < 4; ++x) y2 += 0.5f * (fs[x] * fs[x] - fq[x]) * wc[x];
+      }
+    }
+    __syncthreads();
+  };
+  for (int c = 0; c < nc0; c += 2) {
+    chunk0(c, ea, eb);
+    if (c + 1 < nc0) chunk0(c + 1, eb, ea);
+  }
+
+  // ----- layers 1..L-1: the previous layer's fp32 output is the B operand -----
+  f32x4 X[T16];
+  int g = nc0;
+  for (int i = 1; i < L; ++i) {
+    const float* bli = blv + (i - 1) * NR;
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)   // relu after every layer (DFM.py:128)
+        X[t][x] = fmaxf(acc[t][x] + bli[16 * t + 4 * kq + x], 0.f);
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < TM; ++c, ++g) {   // chunk c = input tiles 2c, 2c+1
+      const int b = g & 1;
+      if (g + 1 < nchunks) dma(g + 1, b ^ 1);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float bv[4] = {X[2 * c + s][0], X[2 * c + s][1], X[2 * c + s][2], X[2 * c + s][3]};
+        step(b, s, bv);
+      }
+      __syncthreads();
+    }
+  }
+
+  const float* blL = blv + (L - 1) * NR;
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < T16; ++t)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int n = 16 * t + 4 * kq + x;
+      part += fmaxf(acc[t][x] + blL[n], 0.f) * vl[n];
+    }
+  part += __shfl_xor(part, 16, kWave);
+  part += __shfl_xor(part, 32, kWave);
+  y2 += __shfl_xor(y2, 16, kWave);
+  y2 += __shfl_xor(y2, 32, kWave);
+  const int64_t m = m0 + myrow;
+  if (kq == 0 && m < a.B) {
+    float y1 = 0.f;
+    for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
+    a.out[m] = ((y1 + y2) + a.bp) + part;
+  }
+}
+
 static int fused_tm(int maxT) {
   const int tms[] = {2, 4, 5, 7, 8, 10, 13};
   for (int t : tms)
@@ -363,18 +595,21 @@ bool dfm_fused_eligible(int L, const int32_t* dims) {
 
 // workspace for the packed weights; an upper bound over F·k <= 16·512 so the
 // size is known from (nlayers, dims) alone
-size_t dfm_fused_pack_bytes(int L, const int32_t* dims) {
+size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16) {
   const int TM = fused_tm(fused_max_tiles(L, dims));
-  const int nc0 = (kFusedMaxF * kFusedMaxK / 16 + 3) / 4;
-  return (size_t)(nc0 + (L - 1) * ((TM + 1) / 2)) * 32 * TM * 8 * 16;
+  const int nc0 = mlp_bf16 ? (kFusedMaxF * kFusedMaxK / 16 + 3) / 4
+                           : (kFusedMaxF * kFusedMaxK / 16 + 1) / 2;
+  const int nch = mlp_bf16 ? (TM + 1) / 2 : TM;
+  return (size_t)(nc0 + (L - 1) * nch) * 32 * TM * 8 * 16;
 }
 
 // returns false when the shape is outside the fused kernel's envelope
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
-                      bool tbf, const float* w, int L, const int32_t* dims,
+                      bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, hipStream_t st) {
-  if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k % 16 || k > kFusedMaxK) return false;
+  if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
+  if (k % 16) return false;
   for (int i = 0; i < L; ++i)
     if (reinterpret_cast<uintptr_t>(Wt[i]) & 15) return false;
   const int TM = fused_tm(fused_max_tiles(L, dims));
@@ -390,12 +625,37 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   }
   a.Wp = Wp; a.bp = bp; a.out = out;
   a.packed = reinterpret_cast<const uint4*>(pack_ws);
+  if (!mlp_bf16) {
+    const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
+    const int nc0 = (F * (k / 16) + 1) / 2;
+    const int64_t units = (int64_t)(nc0 + (L - 1) * TM) * 32 * TM * 8;
+    const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+    hipLaunchKernelGGL(dfm_pack_weights_f32, dim3(pblocks), dim3(256), 0, st, a, TM, nc0,
+                       reinterpret_cast<uint4*>(pack_ws));
+#define HHFM_FUSED32(T)                                                                  \
+  case T:                                                                                \
+    if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T>), grid, dim3(256), 0, st, a);    \
+    else hipLaunchKernelGGL((dfm_fused_f32<false, T>), grid, dim3(256), 0, st, a);       \
+    break;
+    switch (TM) {
+      HHFM_FUSED32(2)
+      HHFM_FUSED32(4)
+      HHFM_FUSED32(5)
+      HHFM_FUSED32(7)
+      HHFM_FUSED32(8)
+      HHFM_FUSED32(10)
+      HHFM_FUSED32(13)
+      default: return false;
+    }
+#undef HHFM_FUSED32
+    return true;
+  }
+  const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
   const int nS = F * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;
   const int64_t units = (int64_t)(nc0 + (L - 1) * NC) * 32 * TM * 8;
   const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
   hipLaunchKernelGGL(dfm_pack_weights, dim3(pblocks), dim3(256), 0, st, a, TM, nc0, NC,
                      reinterpret_cast<uint4*>(pack_ws));
-  const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
 #define HHFM_FUSED(T)                                                                    \
   case T:                                                                                \
     if (tbf) hipLaunchKernelGGL((dfm_fused<true, T>), grid, dim3(256), 0, st, a);        \

@@ -25,9 +25,9 @@
 namespace hhfm {
 
 bool dfm_fused_eligible(int L, const int32_t* dims);
-size_t dfm_fused_pack_bytes(int L, const int32_t* dims);
+size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
-                      bool tbf, const float* w, int L, const int32_t* dims,
+                      bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, hipStream_t st);
 
@@ -129,8 +129,8 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   p.off_h0 = off; off += al256((size_t)B * p.maxL * esz);
   p.off_h1 = off; off += al256((size_t)B * p.maxL * esz);
   p.off_pack = off;
-  if (mlp_dtype == HHFM_BF16 && dfm_fused_eligible(nlayers, dims))
-    off += al256(dfm_fused_pack_bytes(nlayers, dims));
+  if (dfm_fused_eligible(nlayers, dims))
+    off += al256(dfm_fused_pack_bytes(nlayers, dims, mlp_dtype == HHFM_BF16));
   p.total = off;
   return p;
 }
@@ -154,16 +154,15 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
                             float bp, float* out, char* ws, const DfmPlan& p, hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
-  // bf16 MLP: one fused kernel per 128-row block when the shape fits
-  // (dfm_fused.hip); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
+  // One fused kernel per 128-row block when the shape fits (dfm_fused.hip,
+  // bf16 or fp32 MLP); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
   static const bool layered = [] {
     const char* e = getenv("HHFM_DFM_LAYERED");
     return e && e[0] == '1';
   }();
-  if (bf && !layered &&
-      p.total > p.off_pack &&
-      dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, w, nlayers, dims, Wt, bias, Wp,
-                       bp, out, ws + p.off_pack, st))
+  if (!layered && p.total > p.off_pack &&
+      dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
+                       Wp, bp, out, ws + p.off_pack, st))
     return (int)hipGetLastError();
   float* base = reinterpret_cast<float*>(ws + p.off_base);
   float* part = reinterpret_cast<float*>(ws + p.off_part);

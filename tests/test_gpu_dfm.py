@@ -163,13 +163,16 @@ def test_topk_dense_matches_sort():
     (5, 64, [64, 64, 64, 64, 64], "f32", 257),  # layered fallback: 5 layers
     (5, 40, [100], "f32", 77),                  # layered fallback: k % 16 != 0
 ])
-def test_dfm_bf16_envelope(F, k, layers, tdt, B):
-    """bf16 MLP: the fused per-row-block kernel (dfm_fused.hip) and the
-    layer-by-layer GEMM path, both against the bf16-rounding oracle."""
+@pytest.mark.parametrize("mlp", ["bf16", "f32"])
+def test_dfm_fused_envelope(F, k, layers, tdt, B, mlp):
+    """The fused per-row-block kernels (dfm_fused.hip, bf16 and fp32 MLP) and
+    the layer-by-layer GEMM path outside their envelope, against the oracle
+    (bf16: the bf16-rounding oracle, 5e-3; fp32: the reference graph, 2e-5)."""
     rng = np.random.default_rng(F * 1000 + k)
     M = 997
     tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
-    m = _model((100, 200, M, F, k, layers), mlp_dtype=torch.bfloat16, table_dtype=tdtype)
+    mdt = torch.bfloat16 if mlp == "bf16" else torch.float32
+    m = _model((100, 200, M, F, k, layers), mlp_dtype=mdt, table_dtype=tdtype)
     X = rng.integers(0, M, size=(B, F)).astype(np.int32)
     W = m.get_weights()
     L = len(layers)
@@ -180,6 +183,10 @@ def test_dfm_bf16_envelope(F, k, layers, tdt, B):
         E = bf16_round(E)
     Wp, bp = W["concat_projection"], float(W["concat_bias"])
     got = m.score_rows(X)[:, 0]
-    ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
     mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
-    assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
+    if mlp == "bf16":
+        ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+        assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
+    else:
+        ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
+        assert np.all(np.abs(got - ref) <= 2e-5 * mag), np.max(np.abs(got - ref) / mag)
