@@ -50,15 +50,21 @@ __global__ __launch_bounds__(256) void afm_rows_finish(
     const float s = group_sum<kWave>(e);
     const float att = e / s;                      // tf.nn.softmax(axis=1), AFM.py:125
     float bil = 0.f;
-    for (int c = l; c < k; c += kWave) {
+    // uniform loop: every lane takes part in the shuffles (att of pair p
+    // lives in lane p, which may lie beyond k)
+    for (int c0 = 0; c0 < k; c0 += kWave) {
+      const int c = c0 + l;
+      const bool in = c < k;
       float afm = 0.f;
       for (int p = 0; p < np; ++p) {
         int i, j;
         pair_ij(p, F, i, j);
         const float ap = __shfl(att, p, kWave);
-        afm += ap * (tab(E, t_bf16, clamp_id(x[i], M), k, c) * tab(E, t_bf16, clamp_id(x[j], M), k, c));
+        if (in)
+          afm += ap * (tab(E, t_bf16, clamp_id(x[i], M), k, c) *
+                       tab(E, t_bf16, clamp_id(x[j], M), k, c));
       }
-      bil += afm * P[c];                          // AFM·P (AFM.py:138-139)
+      if (in) bil += afm * P[c];                  // AFM·P (AFM.py:138-139)
     }
     bil = group_sum<kWave>(bil);
     if (l == 0) {
@@ -203,7 +209,11 @@ __global__ __launch_bounds__(256) void afm_rows_fused(
       num = fmaf(ee, __shfl(sP, base + q, kWave), num);
     }
     float fb = 0.f;
-    for (int f = 0; f < F; ++f) fb += __shfl(wf, base + f, kWave);
+    if (np >= F) {   // the row's lanes fetched one field each
+      for (int f = 0; f < F; ++f) fb += __shfl(wf, base + f, kWave);
+    } else {         // F = 2: one lane per row
+      for (int f = 0; f < F; ++f) fb += ok ? w[clamp_id(idx[row * F + f], M)] : 0.f;
+    }
     if (ok && p == 0 && h == 0) out[row] = (num / se + fb) + w0;   // add_n, AFM.py:142
   }
 }

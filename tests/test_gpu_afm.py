@@ -79,3 +79,32 @@ def test_afm_catalog_query_chunks():
     res = [ops.afm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, b, p, P,
                                 nu, ni, 20, 0, mc)[1].cpu().numpy() for mc in (1 << 17, 4 * 32 * 5)]
     assert np.array_equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("F,k,A,tdt,B", [
+    (2, 16, 8, "f32", 1),        # fused: one pair per row, 32 rows per MFMA block
+    (3, 48, 40, "bf16", 257),    # fused: NT=2, bf16 table, ragged rows
+    (7, 32, 96, "f32", 1001),    # fused: 21 pairs, NT=3
+    (8, 64, 64, "bf16", 130),    # fused: 28 pairs (largest that fits 32 columns)
+    (9, 32, 32, "f32", 300),     # GEMM path: 36 pairs > 32
+    (5, 20, 16, "f32", 77),      # GEMM path: k % 8 != 0
+])
+def test_afm_rows_envelope(F, k, A, tdt, B):
+    """A1 across the fused kernel's envelope (F <= 8, k % 8 == 0) and the
+    GEMM path beyond it, fp32 and bf16 tables, against the oracle."""
+    from tests.helpers import bf16_round
+    rng = np.random.default_rng(F * 100 + k)
+    M = 811
+    tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
+    m = _afm(50, 700, M, k, A, F=F, table_dtype=tdtype)
+    W = m.get_weights()
+    W["feature_bias"] = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    m.set_weights(feature_bias=W["feature_bias"])
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    E = W["feature_embeddings"]
+    if tdt == "bf16":
+        E = bf16_round(E)
+    args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
+    ref = orc.afm_out(X, E, W["feature_bias"][:, 0], 0.0, *args)[:, 0]
+    got = m.score_rows(X)[:, 0]
+    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
