@@ -468,7 +468,8 @@ extern "C" int hhfm_catalog_topk(
   int32_t* gthr = reinterpret_cast<int32_t*>(ws + p.off_thr);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // 0x80808080 decodes to ~-3.4e38: below every finite score
-  hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
+  const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
+  if (me != hipSuccess) return (int)me;
   const char* Eb = reinterpret_cast<const char*>(E);
 
   {

@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
   }
 }
 
-static void launch_gemm(const GemmArgs& g, bool bf, int epi, hipStream_t st) {
+static inline void launch_gemm(const GemmArgs& g, bool bf, int epi, hipStream_t st) {
   dim3 grid((unsigned)((g.M + GBM - 1) / GBM), (unsigned)((g.N + GBN - 1) / GBN));
   if (epi == 2) {  // grouped dot (AFM attention logits), f32 only
     hipLaunchKernelGGL((gemm_mfma<false, 2>), grid, dim3(256), 0, st, g);
