@@ -113,3 +113,45 @@ def sharded_model_topk(model, A, tp, group=None) -> np.ndarray:
     ranks of ``group`` (every rank calls it with the same A)."""
     _, ids = sharded_topk(A, int(tp), model.n_item, model_scorer(model), group)
     return ids.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# Row-sharded per-triple metrics (SURVEY §8e: "the only collective is a
+# scalar all-reduce of metric sums")
+# ---------------------------------------------------------------------------
+def sharded_evaluate_auc(tr, data1, group=None) -> float:
+    """Train.evaluate_AUC (FM.py:296-324; OurModel7.py:430-461 first-chunk
+    variant) with the scoring split over the ranks: every rank draws the
+    SAME negatives (identical numpy RNG stream, cheap host work), scores only
+    its contiguous slice of each 600-row chunk on its own GPU, and one
+    all-reduce of (hits, comparisons) yields exactly the single-device value
+    (mean of the same booleans)."""
+    from .harness import partition_all
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    dat = data1.values
+    if tr.auc_label_filter:
+        dat = dat[dat[:, 0] > 0]
+    X = np.array(dat[:, 1:], dtype=np.int64)
+    hits, total = 0, 0
+    for chunk in partition_all(600, range(len(X))):
+        pos = X[chunk]
+        negs = tr.sample_negative(pos, 50)          # same draw on every rank
+        b, e = shard_range(len(pos), world, rank)
+        if e > b:
+            mine = pos[b:e]
+            neg = np.repeat(mine[:, None, :], 50, axis=1).reshape(-1, pos.shape[1])
+            neg[:, 1] = negs[b:e].reshape(-1)
+            neg_score = np.asarray(tr.model.score_rows(neg)).reshape(-1)
+            pos_score = np.repeat(np.asarray(tr.model.score_rows(mine)).reshape(-1), 50)
+            hits += int((pos_score > neg_score).sum())
+            total += pos_score.size
+        if tr.auc_first_chunk_only:
+            break
+    t = torch.tensor([hits, total], dtype=torch.float64)
+    if world > 1:
+        backend = dist.get_backend(group)
+        if backend == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t[0] / t[1])

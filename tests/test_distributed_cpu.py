@@ -66,3 +66,42 @@ def test_shard_range_partition():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
             assert max(e - b for b, e in rs) - min(e - b for b, e in rs) <= 1
+
+
+def _auc_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import json
+    from hhfm_amd.NewLoadData import LoadData
+    from tests.test_harness import G, OracleModel, make
+    np.random.seed(2016)
+    d = LoadData(G + "/", "synth_frappe")
+    arr = np.load(os.path.join(G, "harness.npz"))
+    with open(os.path.join(G, "harness.json")) as f:
+        ref = json.load(f)
+    m = OracleModel(arr["E"], arr["w"], d.n_user, d.n_item)
+    np.random.seed(13)
+    a_fm = hd.sharded_evaluate_auc(make(d, m), d.Test_data)
+    mh = OracleModel(arr["E"], arr["w"], d.n_user, d.n_item, fm_scores=False)
+    np.random.seed(17)
+    a_h = hd.sharded_evaluate_auc(make(d, mh, auc_first_chunk_only=True, auc_label_filter=False),
+                                  d.Train_data)
+    if rank == 0:
+        q.put((a_fm == ref["fm_auc_test"], a_h == ref["hhfm_auc_train"]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_auc_gloo(world):
+    """Row-sharded evaluate_AUC + one scalar all-reduce == the reference
+    harness's AUC (fixture), FM and HHFM first-chunk variants."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_auc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) == (True, True)
