@@ -21,7 +21,7 @@
 //  3. topk_merge: per query, merge the S split lists (and, multi-GPU, the R
 //     rank lists gathered over RCCL) into the final top-K.
 // Order everywhere: score descending, item index ascending (tf.nn.top_k).
-#include "topk_common.h"
+#include "gemm_mfma.h"
 
 namespace hhfm {
 
@@ -343,8 +343,19 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 struct Plan {
   int64_t Bpad;
   int nqb, S, tiles_per_split;
-  size_t off_H, off_cst, off_thr, off_ps, off_pi, total;
+  bool dense;            // small catalog: score matrix + dense top-K
+  int64_t ldsc;
+  size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, total;
 };
+
+// Small catalogs (evaluate_TopK over Frappe's 4,082 items is the case): the
+// fused kernel's per-split top-K warm-up dominates when every split holds only
+// a few tiles, so score the whole [B, N] matrix with the MFMA GEMM (fp32
+// 16x16x4, bf16 tables widened on load) and select with one wave per query
+// (hhfm_topk_dense).  Chosen by size alone, so the workspace query agrees.
+static bool dense_catalog(int64_t B, int32_t N) {
+  return N <= 16384 && (int64_t)B * N <= (int64_t)64 << 20;
+}
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -374,6 +385,10 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   } else {
     p.off_pi = off;
   }
+  p.dense = dense_catalog(B, N);
+  p.ldsc = (N + 3) & ~3;
+  p.off_sc = off;
+  if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
   p.total = off;
   return p;
 }
@@ -483,6 +498,27 @@ extern "C" int hhfm_catalog_topk(
       hipLaunchKernelGGL(catalog_queries<false>, dim3((int)blocks), dim3(256), 0, st,
                          qidx, B, p.Bpad, ncols, mode, user_col, ctx_begin,
                          ctx_end, time_begin, time_end, Eb, features_M, k, H, cst);
+  }
+
+  if (p.dense) {
+    float* sc = reinterpret_cast<float*>(ws + p.off_sc);
+    GemmArgs g{};
+    g.M = B;
+    g.N = item_count;
+    g.K = k;
+    g.A = H;
+    g.lda = k;
+    g.Bt = Eb + (int64_t)item_row_begin * k * (bf16 ? 2 : 4);
+    g.ldb = k;
+    g.b_src_bf16 = bf16;
+    const bool fmm = mode == HHFM_MODE_FM;
+    g.bias = (fmm && w) ? w + item_row_begin : nullptr;   // w_item   FM.py:184
+    g.rowbias = fmm ? cst : nullptr;                      // (u+f)·f  FM.py:178-183
+    g.C = sc;
+    g.ldc = p.ldsc;
+    launch_gemm(g, false, 0, st);
+    launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st);
+    return (int)hipGetLastError();
   }
 
   float* os;

@@ -31,6 +31,8 @@ struct GemmArgs {
   int F, kf, t_bf16;    // table row width / dtype
   const void* Bt;       // weights, transposed: [N][ldb] (K contiguous), compute dtype
   int64_t ldb;
+  int b_src_bf16;       // Bt stored as bf16 while computing in f32
+  const float* rowbias; // epilogue 0: added to every element of row m (or null)
   const float* bias;    // [N] or null
   int relu;
   void* C;              // epilogue store: [M][ldc]
@@ -122,6 +124,12 @@ template <bool BF>
 HHFM_DEV u32x4_t load_b_chunk(const GemmArgs& g, int n, int kk) {
   u32x4_t z = {0, 0, 0, 0};
   if (n >= g.N || kk >= g.K) return z;
+  if (!BF && g.b_src_bf16) {  // 4 bf16 -> 4 f32
+    const uint2 x = *reinterpret_cast<const uint2*>(
+        reinterpret_cast<const uint16_t*>(g.Bt) + (int64_t)n * g.ldb + kk);
+    u32x4_t r = {x.x << 16, x.x & 0xffff0000u, x.y << 16, x.y & 0xffff0000u};
+    return r;
+  }
   const char* p = reinterpret_cast<const char*>(g.Bt) + ((int64_t)n * g.ldb + kk) * (BF ? 2 : 4);
   return *reinterpret_cast<const u32x4_t*>(p);
 }
@@ -226,6 +234,7 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
           const int64_t m = m0 + wm * 64 + 16 * a + rq + r;
           if (m < g.M && n < g.ldc) {
             float v = acc[a][b][r] + bn;
+            if (g.rowbias) v += g.rowbias[m];
             if (g.relu) v = fmaxf(v, 0.f);
             if (n >= g.N) v = 0.f;  // zero pad columns: next layer's K padding
             if (g.c_bf16)

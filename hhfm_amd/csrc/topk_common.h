@@ -153,4 +153,17 @@ __global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict
   }
 }
 
+static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds, int K,
+                              int32_t base, float* os, int32_t* oi, hipStream_t st) {
+  int64_t blocks = (B + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  if (K <= 32)
+    hipLaunchKernelGGL(topk_dense_kernel<32>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+                       K, base, os, oi);
+  else
+    hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+                       K, base, os, oi);
+}
+
 }  // namespace hhfm

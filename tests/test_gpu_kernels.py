@@ -151,6 +151,37 @@ def test_catalog_topk_fm_parity(dtype, k):
     _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
 
 
+@pytest.mark.parametrize("mode", ["hhfm", "fm"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k,K", [(32, 1), (128, 20), (64, 64)])
+def test_catalog_topk_streaming_path(mode, dtype, k, K):
+    """Catalogs above the small-catalog bound (N > 16384) take the streaming
+    threshold kernel; the 4082-item cases above take the dense score matrix."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(17 + k + K)
+    n_user, n_item = 300, 20000
+    A, M = synth_rows(rng, 70, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    if mode == "hhfm":
+        s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, n_user, n_item, 0,
+                                None, 0, (2, 5), (0, 0))
+        ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
+        scale = _hhfm_scale(A, E, n_user, n_item)
+    else:
+        w = rng.normal(0, 0.01, size=M).astype(np.float32)
+        s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_FM, K, n_user, n_item, 0,
+                                _dev(w), 0, (2, 5), (0, 0))
+        ref = orc.fm_catalog_scores(A, E, w, n_user, n_item)
+        f = E[A[:, 2:].astype(np.int64)].sum(1)
+        q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
+        it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
+        scale = (q @ it.T + (q * np.abs(f)).sum(1, keepdims=True)).max(1, keepdims=True) + 0.05
+    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale)
+
+
 def test_catalog_topk_large_catalog_shard_offsets():
     """Many splits (merge path) + a shard with non-zero row/global base."""
     from hhfm_amd import ops
