@@ -52,6 +52,30 @@ def test_fm_score_rows_parity(dtype, k, F):
     assert np.all(np.abs(got - ref) <= RTOL * scale + 1e-12)
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k,F", [(64, 5), (16, 3), (128, 12), (16, 8)])
+def test_fm_score_rows_flag_variants_bit_identical(dtype, k, F):
+    """HHFM_FLAG_STREAM_TABLE changes only how the bytes move: same bits."""
+    from hhfm_amd._native import native
+    rng = np.random.default_rng(77 + k + F)
+    B, M = 10007, 50000
+    X = _dev(rng.integers(0, M, size=(B, F)).astype(np.int32))
+    E = _dev(table(rng, M, k))
+    if dtype == "bf16":
+        E = E.to(torch.bfloat16)
+    w = _dev(rng.normal(0, 0.01, size=M).astype(np.float32))
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for flags in (0, 1):
+        o = torch.full((B,), float("nan"), device="cuda")
+        native().fm_score_rows_ex(X.data_ptr(), B, F, E.data_ptr(), M, k,
+                                  1 if dtype == "bf16" else 0, w.data_ptr(), 0.003,
+                                  o.data_ptr(), flags, st)
+        outs.append(o.cpu())
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+
+
 @pytest.mark.parametrize("B", [0, 1, 7, 63, 1000])
 def test_fm_score_rows_ragged_and_generic(B):
     """Odd B, and k=20 (not 16-B aligned rows -> generic kernel), no w."""
