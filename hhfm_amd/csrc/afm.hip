@@ -15,6 +15,8 @@
 // afm_cat_finish forms the exp-weighted score of AFM.py:232-243 and
 // hhfm_topk_dense selects.  The reference's raw exp (no max subtraction,
 // AFM.py:223,230) is kept.
+#include <cstdlib>
+
 #include "gemm_mfma.h"
 
 namespace hhfm {
@@ -227,7 +229,7 @@ __global__ __launch_bounds__(64) void afm_cat_prep(
     int64_t M, int k, const float* __restrict__ Wt, const float* __restrict__ ab,
     const float* __restrict__ ap, int A, const float* __restrict__ P,
     float* __restrict__ W2, float* __restrict__ D, float* __restrict__ ufdot,
-    float* __restrict__ suma) {
+    float* __restrict__ suma, int emit_w2) {
   __shared__ float uf[kAfmMaxUF][kAfmMaxK];
   __shared__ float pr[kAfmMaxK];
   const int l = threadIdx.x;
@@ -277,6 +279,7 @@ __global__ __launch_bounds__(64) void afm_cat_prep(
     suma[b] = sa;
   }
   // W''[(b*uF+f)*A + a][c] = uf_f[c] * W[c][a];  D[b*uF+f][c] = P[c]*uf_f[c]
+  if (!emit_w2) return;
   for (int f = 0; f < uF; ++f) {
     for (int a = 0; a < A; ++a) {
       float* dst = W2 + ((b * uF + f) * (int64_t)A + a) * k;
@@ -318,15 +321,174 @@ __global__ __launch_bounds__(256) void afm_cat_finish(
   scores[b * N + i] = num / den + w[id];           // score3 + bias, AFM.py:239-243
 }
 
+// ---- A2 fused: wave = one query x 32-item tiles, lane column = item ----------
+// The item-side logit of (query, item, field f) is Σ_a p_a·relu((uf_f ⊙ item)·W
+// + b)_a (AFM.py:227-230): the A1 kernel's transposed product with the pair
+// product uf_f ⊙ item formed in registers (uf_f broadcast from LDS, the item
+// row streamed from HBM one 8-k step ahead), the shared Wᵀ image as the A
+// operand.  Per field the lane also forms P·(uf_f ⊙ item); the score
+// (P·ufw + Σ_f e^lg_f P·(uf_f ⊙ item)) / (Σa_uf + Σ_f e^lg_f) + w_item
+// (AFM.py:232-243) is written once per (query, item) for hhfm_topk_dense.
+constexpr int kAfmCatFusedMaxUF = 7;
+
+template <bool TBF, int NT>
+__global__ __launch_bounds__(256) void afm_cat_fused(
+    const int32_t* __restrict__ q, int64_t nq, int F, const void* __restrict__ E, int64_t M,
+    int k, const float* __restrict__ Wt, const float* __restrict__ att_b,
+    const float* __restrict__ att_p, int A, const float* __restrict__ P,
+    const float* __restrict__ ufdot, const float* __restrict__ suma, int64_t item_row_begin,
+    int32_t N, int tiles_per_block, int nchunk, const float* __restrict__ w,
+    float* __restrict__ scores) {
+  constexpr int NA = NT * 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_cat_fused_lds()
+  float4* img = reinterpret_cast<float4*>(smem);
+  float* Pl = smem + NA * k;
+  float* bl = Pl + kAfmMaxK;
+  float* apl = bl + NA;
+  float* ufl = apl + NA;                     // [4 waves][uF][k]
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int j = l & 31, h = l >> 5;
+  const int uF = F - 1;
+  const int U = k / 4;
+  int sw = 1;
+  while (sw < 16 && U % (2 * sw) == 0) sw *= 2;
+  const int SW = sw - 1;
+  const int64_t qg = blockIdx.x / nchunk;
+  const int chunk = (int)(blockIdx.x - qg * nchunk);
+  for (int x = tid; x < NA * U; x += 256) {
+    const int u = x / U, c = x - u * U;
+    const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    img[u * U + (c ^ (u & SW))] = v;
+  }
+  for (int x = tid; x < k; x += 256) Pl[x] = P[x];
+  for (int x = tid; x < NA; x += 256) {
+    bl[x] = x < A ? att_b[x] : 0.f;
+    apl[x] = x < A ? att_p[x] : 0.f;
+  }
+  // uf of the 4 queries: [E[q0], E[q2], ..., E[q_{F-1}]]  (AFM.py:210-212)
+  for (int x = tid; x < 4 * uF * k; x += 256) {
+    const int qq = x / (uF * k), r = x - qq * uF * k, f = r / k, c = r - f * k;
+    const int64_t b = qg * 4 + qq;
+    float v = 0.f;
+    if (b < nq) v = tab(E, TBF, clamp_id(q[b * F + (f == 0 ? 0 : f + 1)], M), k, c);
+    ufl[x] = v;
+  }
+  __syncthreads();
+
+  const int64_t b = qg * 4 + wv;
+  if (b >= nq) return;
+  const float* uq = ufl + wv * uF * k;
+  const float ud = ufdot[b], sa = suma[b];
+  const int KQ = k / 8;
+  const int S = uF * KQ;
+  const int ntile = (N + 31) / 32;
+  const int t0 = chunk * tiles_per_block;
+  const int t1 = min(t0 + tiles_per_block, ntile);
+  for (int tile = t0; tile < t1; ++tile) {
+    const int32_t item = tile * 32 + j;
+    const bool ok = item < N;
+    const int64_t id = item_row_begin + (ok ? item : 0);
+    auto gather = [&](int t) -> float4 {
+      const int c0 = 8 * t + 4 * h;
+      if constexpr (TBF) {
+        const uint2 u = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const uint16_t*>(E) + id * k + c0);
+        return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                           __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + id * k + c0);
+      }
+    };
+    f32x16 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int x = 0; x < 16; ++x) acc[n][x] = 0.f;
+    float sP = 0.f, num = 0.f, den = 0.f;
+    float4 xa = gather(0);
+    for (int s = 0, f = 0, t = 0; s < S; ++s) {
+      const float4 xn = (s + 1 < S) ? gather(t + 1 < KQ ? t + 1 : 0) : xa;
+      const int c0 = 8 * t + 4 * h;
+      const float4 ua = *reinterpret_cast<const float4*>(uq + f * k + c0);
+      const float pe[4] = {xa.x * ua.x, xa.y * ua.y, xa.z * ua.z, xa.w * ua.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sP = fmaf(pe[e], Pl[c0 + e], sP);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int u = 32 * n + j;
+        const float4 wa = img[u * U + ((2 * t + h) ^ (u & SW))];
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, pe[0], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, pe[1], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, pe[2], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, pe[3], acc[n], 0, 0, 0);
+      }
+      xa = xn;
+      if (++t == KQ) {   // field f done: its logit, raw exp (AFM.py:230)
+        float lg = 0.f;
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+#pragma unroll
+          for (int x = 0; x < 16; ++x) {
+            const int u = 32 * n + 8 * (x >> 2) + 4 * h + (x & 3);
+            lg = fmaf(fmaxf(acc[n][x] + bl[u], 0.f), apl[u], lg);
+            acc[n][x] = 0.f;
+          }
+        lg += __shfl_xor(lg, 32, kWave);
+        sP += __shfl_xor(sP, 32, kWave);
+        const float a = expf(lg);
+        num = fmaf(a, sP, num);
+        den += a;
+        sP = 0.f;
+        t = 0;
+        ++f;
+      }
+    }
+    if (ok && h == 0) scores[b * N + item] = (ud + num) / (sa + den) + w[id];
+  }
+}
+
+static size_t afm_cat_fused_lds(int F, int k, int A) {
+  const int NA = (A + 31) / 32 * 32;
+  return 4 * (size_t)(NA * k + kAfmMaxK + 2 * NA + 4 * (F - 1) * k);
+}
+
+// fused A2 envelope: Wᵀ padded to NT*32 <= 128 rows, <= 7 query fields, the
+// Wᵀ image and the 4 queries' fields in <= 64 KB of LDS; HHFM_AFM_CATALOG_GEMM=1 forces the GEMM path.
+static bool afm_cat_fused_ok(int F, int k, int A) {
+  static const bool gemm = [] {
+    const char* e = getenv("HHFM_AFM_CATALOG_GEMM");
+    return e && e[0] == '1';
+  }();
+  const int NT = (A + 31) / 32;
+  return !gemm && F - 1 <= kAfmCatFusedMaxUF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 &&
+         afm_cat_fused_lds(F, k, A) <= 65536;   // default dynamic-LDS limit
+}
+
 struct AfmCatPlan {
   int64_t qc;
   int G;
+  bool fused;
   size_t off_W2, off_D, off_ud, off_sa, off_part, off_sc, total;
 };
 
 static AfmCatPlan afm_cat_plan(int64_t B, int F, int k, int A, int N, int64_t max_cols) {
   AfmCatPlan p{};
   const int uF = F - 1;
+  p.fused = afm_cat_fused_ok(F, k, A);
+  if (p.fused) {   // only Σa_uf, P·ufw and the [qc, N] score block
+    int64_t qc = max_cols / ((int64_t)uF * A);
+    if (qc < 1) qc = 1;
+    if (qc > B) qc = B;
+    p.qc = qc;
+    size_t off = 0;
+    p.off_W2 = p.off_D = p.off_part = 0;
+    p.off_ud = off; off += a256((size_t)qc * 4);
+    p.off_sa = off; off += a256((size_t)qc * 4);
+    p.off_sc = off; off += a256((size_t)qc * N * 4);
+    p.total = off;
+    return p;
+  }
   p.G = A < 64 ? A : 64;
   int64_t qc = max_cols / ((int64_t)uF * A);
   if (qc < 1) qc = 1;
@@ -446,7 +608,9 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   if (item_count < 1 || item_row_begin < 0 || (int64_t)item_row_begin + item_count > features_M)
     return HHFM_EINVAL;
   if (K < 1 || K > item_count) return HHFM_EINVAL;
-  if (K > 64 || k % 4 || A % 16 || (A > 64 && A % 64)) return HHFM_EUNSUPPORTED;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  if (!afm_cat_fused_ok(F, k, A) && (k % 4 || A % 16 || (A > 64 && A % 64)))
+    return HHFM_EUNSUPPORTED;
   if (B == 0) return HHFM_OK;
   if (!qidx || !E || !w || !Wt || !att_b || !att_p || !P || !top_score || !top_idx)
     return HHFM_EINVAL;
@@ -465,29 +629,58 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   for (int64_t b0 = 0; b0 < B; b0 += p.qc) {
     const int64_t nq = (B - b0) < p.qc ? (B - b0) : p.qc;
     hipLaunchKernelGGL(afm_cat_prep, dim3((unsigned)nq), dim3(64), 0, st, qidx + b0 * F, nq, F,
-                       E, tb, features_M, k, Wt, att_b, att_p, A, P, W2, D, ud, sa);
-    GemmArgs g{};
-    g.M = item_count;
-    g.N = (int)(nq * uF * A);
-    g.K = k;
-    g.A = reinterpret_cast<const char*>(E) + (int64_t)item_row_begin * k * (tb ? 2 : 4);
-    g.lda = k;
-    g.a_src_bf16 = tb;
-    g.Bt = W2;
-    g.ldb = k;
-    g.bias = att_b;
-    g.relu = 1;
-    g.dotv = att_p;
-    g.partial = part;
-    g.G = p.G;
-    g.mod = A;
-    g.ldp = nq * uF * A / p.G;
-    launch_gemm(g, false, 2, st);
-    const int64_t nblk = (item_count + kWave - 1) / kWave;
-    const int64_t waves = nq * nblk;
-    hipLaunchKernelGGL(afm_cat_finish, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, nq,
-                       uF, A, p.G, part, g.ldp, D, ud, sa, E, tb, k, (int64_t)item_row_begin,
-                       item_count, w, sc);
+                       E, tb, features_M, k, Wt, att_b, att_p, A, P, W2, D, ud, sa,
+                       (int)!p.fused);
+    if (p.fused) {
+      const int64_t qgroups = (nq + 3) / 4;
+      const int ntile = (item_count + 31) / 32;
+      int64_t nchunk = (2048 + qgroups - 1) / qgroups;
+      if (nchunk > ntile) nchunk = ntile;
+      const int tpb = (int)((ntile + nchunk - 1) / nchunk);
+      nchunk = (ntile + tpb - 1) / tpb;
+      const dim3 grid((unsigned)(qgroups * nchunk));
+      const int NT = (A + 31) / 32;
+      const size_t lds = afm_cat_fused_lds(F, k, A);
+#define HHFM_AFM_CAT_FUSED(N)                                                               \
+  if (NT == N) {                                                                           \
+    if (tb)                                                                                \
+      hipLaunchKernelGGL((afm_cat_fused<true, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, F, \
+                         E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                   \
+                         (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
+    else                                                                                   \
+      hipLaunchKernelGGL((afm_cat_fused<false, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, \
+                         F, E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                \
+                         (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
+  }
+      HHFM_AFM_CAT_FUSED(1)
+      HHFM_AFM_CAT_FUSED(2)
+      HHFM_AFM_CAT_FUSED(3)
+      HHFM_AFM_CAT_FUSED(4)
+#undef HHFM_AFM_CAT_FUSED
+    } else {
+      GemmArgs g{};
+      g.M = item_count;
+      g.N = (int)(nq * uF * A);
+      g.K = k;
+      g.A = reinterpret_cast<const char*>(E) + (int64_t)item_row_begin * k * (tb ? 2 : 4);
+      g.lda = k;
+      g.a_src_bf16 = tb;
+      g.Bt = W2;
+      g.ldb = k;
+      g.bias = att_b;
+      g.relu = 1;
+      g.dotv = att_p;
+      g.partial = part;
+      g.G = p.G;
+      g.mod = A;
+      g.ldp = nq * uF * A / p.G;
+      launch_gemm(g, false, 2, st);
+      const int64_t nblk = (item_count + kWave - 1) / kWave;
+      const int64_t waves = nq * nblk;
+      hipLaunchKernelGGL(afm_cat_finish, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, nq,
+                         uF, A, p.G, part, g.ldp, D, ud, sa, E, tb, k, (int64_t)item_row_begin,
+                         item_count, w, sc);
+    }
     int64_t tblocks = (nq + 3) / 4;
     if (tblocks > 4096) tblocks = 4096;
     if (K <= 32)

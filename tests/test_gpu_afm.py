@@ -108,3 +108,37 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     ref = orc.afm_out(X, E, W["feature_bias"][:, 0], 0.0, *args)[:, 0]
     got = m.score_rows(X)[:, 0]
     assert np.allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("F,k,A,tdt,nq,ni,K", [
+    (5, 64, 64, "f32", 37, 1001, 20),     # fused (Frappe shape), ragged last item tile
+    (3, 48, 40, "bf16", 9, 700, 1),       # fused: A padded to 64, bf16 table
+    (8, 32, 96, "f32", 5, 333, 64),       # fused: 7 query fields, NT = 3
+    (4, 16, 8, "bf16", 70, 64, 5),        # fused: one tile pair per query group
+    (9, 32, 32, "f32", 11, 500, 20),      # GEMM path: 8 query fields
+    (5, 20, 16, "f32", 13, 400, 20),      # GEMM path: k % 8 != 0
+    (5, 128, 128, "f32", 6, 300, 20),     # GEMM path: Wᵀ image > 64 KB of LDS
+])
+def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
+    """A2 across the fused kernel's envelope and the GEMM path beyond it."""
+    from tests.helpers import bf16_round
+    rng = np.random.default_rng(F * 1000 + k + A)
+    nu = 60
+    M = nu + ni + 40
+    tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
+    m = _afm(nu, ni, M, k, A, F=F, table_dtype=tdtype)
+    W = m.get_weights()
+    W["feature_bias"] = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    m.set_weights(feature_bias=W["feature_bias"])
+    A_ = np.concatenate([rng.integers(0, nu, (nq, 1)), rng.integers(nu, nu + ni, (nq, 1)),
+                         rng.integers(nu + ni, M, (nq, F - 2))], 1).astype(np.int32)
+    E = W["feature_embeddings"]
+    if tdt == "bf16":
+        E = bf16_round(E)
+    args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
+    sc = orc.afm_catalog_scores(A_, E, W["feature_bias"][:, 0], *args, nu, ni)
+    pred = m.topk(A_, K)
+    rs, ri = orc.top_k(sc, K + 1) if K < ni else orc.top_k(sc, K)
+    mism, amb = orc.topk_index_agreement(rs, ri[:, :K], pred,
+                                         1e-5 * np.abs(sc).max(1, keepdims=True))
+    assert mism == 0, (mism, amb)
