@@ -33,6 +33,7 @@
 // out[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c]) + bp) + Σ_n relu(h_L)·Wp[F+k+n]
 #include "gemm_mfma.h"
 
+
 namespace hhfm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -42,7 +43,6 @@ constexpr int kFusedMaxLayers = 4;
 constexpr int kFusedMaxF = 16;
 constexpr int kFusedMaxK = 512;
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
-constexpr int kFusedMaxSteps = kFusedMaxF * kFusedMaxK / 16 + 4;
 
 struct FusedDfmArgs {
   const int32_t* idx;
@@ -114,16 +114,13 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   constexpr int kW = 2 * CU * 16;
   constexpr int kIds = kW, kBl = kIds + kFusedRows * kFusedMaxF * 4;
   constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
-  constexpr int kSf = kWp + (kFusedMaxF + kFusedMaxK) * 4, kSc = kSf + kFusedMaxSteps * 4;
-  constexpr int kSmem = kSc + kFusedMaxSteps * 4;
+  constexpr int kSmem = kWp + (kFusedMaxF + kFusedMaxK) * 4;
   __shared__ __attribute__((aligned(16))) char smem[kSmem];
   uint4* wbuf0 = reinterpret_cast<uint4*>(smem);   // [2][NR rows][8 slots]
   int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
   float* blv = reinterpret_cast<float*>(smem + kBl);  // [layer][NR]
   float* vl = reinterpret_cast<float*>(smem + kVl);
   float* wpl = reinterpret_cast<float*>(smem + kWp);
-  int32_t* step_f = reinterpret_cast<int32_t*>(smem + kSf);
-  int32_t* step_col = reinterpret_cast<int32_t*>(smem + kSc);
 
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int r = l & 31, h = l >> 5;
@@ -140,13 +137,10 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   for (int i = 0; i < L; ++i)
     for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
   for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
-  for (int x = tid; x < F + k; x += 256) wpl[x] = a.Wp[x];
+  // Wp: [0, F) the Σw weights, [kFusedMaxF, +k) the FM columns (16-B aligned)
+  for (int x = tid; x < F + k; x += 256) wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x];
   // layer-0 K order is c-major: step S covers field S%F, columns 16(S/F)..+15.
   // Padding steps (S >= nS) multiply zero weights and skip the FM part.
-  for (int S = tid; S < 4 * nc0; S += 256) {
-    step_f[S] = S < nS ? S % F : -1;
-    step_col[S] = S < nS ? 16 * (S / F) : 0;
-  }
 
   // chunk g -> LDS buffer b: TM lane-linear 1-KB DMAs per wave
   auto dma = [&](int g, int b) {
@@ -172,9 +166,9 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int S = 4 * c + s;
-      const int f = step_f[S];
-      const int64_t id = ids[myrow * F + (f >= 0 ? f : 0)];
-      const int col = step_col[S] + 8 * h;
+      const bool real = S < nS;                  // padding steps: zero weights
+      const int64_t id = ids[myrow * F + (real ? S % F : 0)];
+      const int col = (real ? 16 * (S / F) : 0) + 8 * h;
       if constexpr (TBF) {
         e.v[s] = *reinterpret_cast<const uint4*>(
             reinterpret_cast<const uint16_t*>(a.E) + id * k + col);
@@ -196,8 +190,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   float y2 = 0.f;
 
   __syncthreads();   // ids, step tables visible
-  EChunk ea, eb;
-  eload(ea, 0);
+  EChunk e0;
+  eload(e0, 0);
   dma(0, 0);
   __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
@@ -229,36 +223,48 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   };
 
   // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
-  auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
+  // Chunk c first turns the embeddings gathered during chunk c-1 into its 4
+  // B operands (and the fp32 values of the FM part), THEN issues chunk c+1's
+  // weight DMA and gathers into the freed registers: the compiler's wait on
+  // the gathered registers (it cannot count loads across the loop's back
+  // edge, so it is a vmcnt(0)) then lands before the new loads, not after.
+  auto chunk0 = [&](int c, EChunk& e) {
     const int b = c & 1;
-    if (c + 1 < nchunks) dma(c + 1, b ^ 1);
-    if (c + 1 < nc0) eload(en, c + 1);
     float v[4][8];
-    auto bop = [&](int j) {
-      uint4 bx;
-      if constexpr (TBF) {
-        bx = e.v[j];
-        const uint32_t x4[4] = {bx.x, bx.y, bx.z, bx.w};
+    uint4 bxs[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[j][2 * q] = __uint_as_float(x4[q] << 16);
-          v[j][2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
-        }
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (TBF) {
+        bxs[j] = e.v[j];   // already the B operand; fp32 values made per step
       } else {
         const uint4 p = e.v[2 * j], q = e.v[2 * j + 1];
         v[j][0] = __uint_as_float(p.x); v[j][1] = __uint_as_float(p.y);
         v[j][2] = __uint_as_float(p.z); v[j][3] = __uint_as_float(p.w);
         v[j][4] = __uint_as_float(q.x); v[j][5] = __uint_as_float(q.y);
         v[j][6] = __uint_as_float(q.z); v[j][7] = __uint_as_float(q.w);
-        bx = make_uint4(pack_bf16x2(v[j][0], v[j][1]), pack_bf16x2(v[j][2], v[j][3]),
-                        pack_bf16x2(v[j][4], v[j][5]), pack_bf16x2(v[j][6], v[j][7]));
+        bxs[j] = make_uint4(pack_bf16x2(v[j][0], v[j][1]), pack_bf16x2(v[j][2], v[j][3]),
+                            pack_bf16x2(v[j][4], v[j][5]), pack_bf16x2(v[j][6], v[j][7]));
       }
-      return __builtin_bit_cast(bf16x8, bx);
+    }
+    // then the next chunk's weight DMA and gathers, in one burst
+    // (measured: placing them one per MFMA gap instead ran 6-7 % slower)
+    if (c + 1 < nchunks) dma(c + 1, b ^ 1);
+    if (c + 1 < nc0) eload(e, c + 1);
+    auto bop = [&](int j) {
+      if constexpr (TBF) {
+        const uint32_t x4[4] = {bxs[j].x, bxs[j].y, bxs[j].z, bxs[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[j][2 * q] = __uint_as_float(x4[q] << 16);
+          v[j][2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
+        }
+      }
+      return __builtin_bit_cast(bf16x8, bxs[j]);
     };
     // FM second-order part over the same values (DFM.py:114-122)
     auto side = [&](int j) {
       const int S = 4 * c + j;
-      const int f = step_f[S];
+      const int f = S < nS ? S % F : -1;
       if (f == 0) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) { fs[q] = 0.f; fq[q] = 0.f; }
@@ -268,19 +274,21 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         fs[q] += v[j][q];
         fq[q] += v[j][q] * v[j][q];
       }
-      if (f == F - 1) {
-        const float* wc = wpl + F + step_col[S] + 8 * h;
+      if (f == F - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
+        const float4* wc =
+            reinterpret_cast<const float4*>(wpl + kFusedMaxF + 16 * (S / F) + 8 * h);
+        const float4 w0 = wc[0], w1 = wc[1];
+        const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        float d = 0.f;
 #pragma unroll
-        for (int q = 0; q < 8; ++q) y2 += 0.5f * (fs[q] * fs[q] - fq[q]) * wc[q];
+        for (int q = 0; q < 8; ++q) d += 0.5f * (fs[q] * fs[q] - fq[q]) * wq[q];
+        y2 += d;
       }
     };
     run_chunk(b, bop, side);
-    __syncthreads();
+    __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
   };
-  for (int c = 0; c < nc0; c += 2) {
-    chunk0(c, ea, eb);
-    if (c + 1 < nc0) chunk0(c + 1, eb, ea);
-  }
+  for (int c = 0; c < nc0; ++c) chunk0(c, e0);
 
   // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
   uint32_t X[TM][8];
@@ -293,10 +301,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     for (int t = 0; t < TM; ++t) {
       float v[16];
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        const int n = 32 * t + 8 * (x >> 2) + 4 * h + (x & 3);
-        v[x] = fmaxf(acc[t][x] + bli[n], 0.f);
-        acc[t][x] = 0.f;
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const float4 bq = *reinterpret_cast<const float4*>(bli + 32 * t + 8 * g4 + 4 * h);
+        const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[4 * g4 + e] = fmaxf(acc[t][4 * g4 + e] + bv[e], 0.f);
+          acc[t][4 * g4 + e] = 0.f;
+        }
       }
 #pragma unroll
       for (int q = 0; q < 8; ++q) X[t][q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
@@ -327,9 +339,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 #pragma unroll
   for (int t = 0; t < TM; ++t)
 #pragma unroll
-    for (int x = 0; x < 16; ++x) {
-      const int n = 32 * t + 8 * (x >> 2) + 4 * h + (x & 3);
-      part += fmaxf(acc[t][x] + blL[n], 0.f) * vl[n];
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int n = 32 * t + 8 * g4 + 4 * h;
+      const float4 bq = *reinterpret_cast<const float4*>(blL + n);
+      const float4 vq = *reinterpret_cast<const float4*>(vl + n);
+      part += fmaxf(acc[t][4 * g4 + 0] + bq.x, 0.f) * vq.x;
+      part += fmaxf(acc[t][4 * g4 + 1] + bq.y, 0.f) * vq.y;
+      part += fmaxf(acc[t][4 * g4 + 2] + bq.z, 0.f) * vq.z;
+      part += fmaxf(acc[t][4 * g4 + 3] + bq.w, 0.f) * vq.w;
     }
   part += __shfl_xor(part, 32, kWave);
   y2 += __shfl_xor(y2, 32, kWave);
