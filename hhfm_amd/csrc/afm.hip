@@ -91,19 +91,29 @@ __global__ __launch_bounds__(256) void afm_rows_finish(
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kAfmMaxK = 256;
 constexpr int kAfmFusedMaxF = 8;     // F(F-1)/2 <= 28 combos of one row fit 32 columns
-constexpr int kAfmFusedImg = 32 * 512;   // floats: NT*32 units x k <= 512*32
+
+// LDS of the fused AFM kernels is sized per call (dynamic); above the default
+// 64 KB a launch must raise the kernel's limit (gfx950: 160 KB per workgroup).
+static void allow_lds(const void* fn, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+static size_t afm_rows_fused_lds(int k, int A) {
+  const int NA = (A + 31) / 32 * 32;
+  return 4 * (size_t)(NA * k + k + 2 * NA);
+}
 
 template <bool TBF, int NT>
-__global__ __launch_bounds__(256) void afm_rows_fused(
+__global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_fused(
     const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
     int k, const float* __restrict__ w, float w0, const float* __restrict__ Wt,
     const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
     const float* __restrict__ P, float* __restrict__ out) {
   constexpr int NA = NT * 32;
-  __shared__ __attribute__((aligned(16))) float smem[kAfmFusedImg + kAfmMaxK + 2 * NA];
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_rows_fused_lds()
   float4* img = reinterpret_cast<float4*>(smem);
-  float* Pl = smem + kAfmFusedImg;
-  float* bl = Pl + kAfmMaxK;
+  float* Pl = smem + NA * k;
+  float* bl = Pl + k;
   float* apl = bl + NA;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int j = l & 31, h = l >> 5;
@@ -131,43 +141,59 @@ __global__ __launch_bounds__(256) void afm_rows_fused(
   const bool live = r < R;
   const int64_t nblk = (B + R - 1) / R;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += wstride) {
+  const int KQ = k / 8;
+  // the lane combo's two table rows in block blk
+  auto ids_of = [&](int64_t blk, int64_t& ia, int64_t& ib) {
+    const int64_t row = blk * R + r;
+    const int64_t rr = (live && row < B) ? row : 0;
+    ia = clamp_id(idx[rr * F + (live ? pi : 0)], M);
+    ib = clamp_id(idx[rr * F + (live ? pj : 1)], M);
+  };
+  // this lane's 4 k of 8-k step t, one step of gathers in flight ahead
+  auto gather = [&](int64_t ia, int64_t ib, int t, float4& x, float4& y) {
+    const int c0 = 8 * t + 4 * h;
+    if constexpr (TBF) {
+      const uint2 u = *reinterpret_cast<const uint2*>(
+          reinterpret_cast<const uint16_t*>(E) + ia * k + c0);
+      const uint2 v = *reinterpret_cast<const uint2*>(
+          reinterpret_cast<const uint16_t*>(E) + ib * k + c0);
+      x = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      y = make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
+                      __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
+    } else {
+      x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ia * k + c0);
+      y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ib * k + c0);
+    }
+  };
+  // The next block's ids are read at the start of this block and its first
+  // step is gathered during this block's last one: the idx -> row dependent
+  // chain never stalls a block start.
+  int64_t blk = (int64_t)blockIdx.x * 4 + wv;
+  int64_t ia = 0, ib = 0;
+  float4 xa = make_float4(0.f, 0.f, 0.f, 0.f), ya = xa;
+  if (blk < nblk) {
+    ids_of(blk, ia, ib);
+    gather(ia, ib, 0, xa, ya);
+  }
+  for (; blk < nblk; blk += wstride) {
     const int64_t row = blk * R + r;
     const bool ok = live && row < B;
-    const int64_t rr = ok ? row : 0;
-    const int64_t ia = clamp_id(idx[rr * F + (live ? pi : 0)], M);
-    const int64_t ib = clamp_id(idx[rr * F + (live ? pj : 1)], M);
+    const bool has_next = blk + wstride < nblk;
+    int64_t na = 0, nb = 0;
+    if (has_next) ids_of(blk + wstride, na, nb);
     f32x16 acc[NT];
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int x = 0; x < 16; ++x) acc[n][x] = 0.f;
     float sP = 0.f;
-    // this lane's 4 k of 8-k step t, one step of gathers in flight ahead
-    auto gather = [&](int t, float4& x, float4& y) {
-      const int c0 = 8 * t + 4 * h;
-      if constexpr (TBF) {
-        const uint2 u = *reinterpret_cast<const uint2*>(
-            reinterpret_cast<const uint16_t*>(E) + ia * k + c0);
-        const uint2 v = *reinterpret_cast<const uint2*>(
-            reinterpret_cast<const uint16_t*>(E) + ib * k + c0);
-        x = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-        y = make_float4(__uint_as_float(v.x << 16), __uint_as_float(v.x & 0xffff0000u),
-                        __uint_as_float(v.y << 16), __uint_as_float(v.y & 0xffff0000u));
-      } else {
-        x = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ia * k + c0);
-        y = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(E) + ib * k + c0);
-      }
-    };
     // Σw of the row: lanes p < F of the row's group fetch one field each
     const float wf = (ok && p < F) ? w[clamp_id(idx[row * F + p], M)] : 0.f;
-    float4 xa, ya;
-    gather(0, xa, ya);
-    const int KQ = k / 8;
     for (int t = 0; t < KQ; ++t) {
       float4 xn = xa, yn = ya;
-      if (t + 1 < KQ) gather(t + 1, xn, yn);
+      if (t + 1 < KQ) gather(ia, ib, t + 1, xn, yn);
+      else if (has_next) gather(na, nb, 0, xn, yn);
       const int c0 = 8 * t + 4 * h;
       const float ea[4] = {xa.x, xa.y, xa.z, xa.w}, eb[4] = {ya.x, ya.y, ya.z, ya.w};
       float pe[4];
@@ -188,6 +214,8 @@ __global__ __launch_bounds__(256) void afm_rows_fused(
       xa = xn;
       ya = yn;
     }
+    ia = na;
+    ib = nb;
     // logit of this lane's combo: Σ_units p·relu(acc + b)  (AFM.py:112-117)
     float lg = 0.f;
 #pragma unroll
@@ -454,7 +482,7 @@ static size_t afm_cat_fused_lds(int F, int k, int A) {
 }
 
 // fused A2 envelope: Wᵀ padded to NT*32 <= 128 rows, <= 7 query fields, the
-// Wᵀ image and the 4 queries' fields in <= 64 KB of LDS; HHFM_AFM_CATALOG_GEMM=1 forces the GEMM path.
+// Wᵀ image and the 4 queries' fields in LDS; HHFM_AFM_CATALOG_GEMM=1 forces the GEMM path.
 static bool afm_cat_fused_ok(int F, int k, int A) {
   static const bool gemm = [] {
     const char* e = getenv("HHFM_AFM_CATALOG_GEMM");
@@ -462,7 +490,7 @@ static bool afm_cat_fused_ok(int F, int k, int A) {
   }();
   const int NT = (A + 31) / 32;
   return !gemm && F - 1 <= kAfmCatFusedMaxUF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 &&
-         afm_cat_fused_lds(F, k, A) <= 65536;   // default dynamic-LDS limit
+         afm_cat_fused_lds(F, k, A) <= 160 * 1024;
 }
 
 struct AfmCatPlan {
@@ -541,12 +569,18 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       int64_t blocks = (nblk + 3) / 4;
       if (blocks > 2048) blocks = 2048;
       const bool tb = dtype == HHFM_BF16;
+      const size_t lds = afm_rows_fused_lds(k, A);
 #define HHFM_AFM_FUSED(N)                                                                   \
   if (NT == N) {                                                                           \
-    if (tb) hipLaunchKernelGGL((afm_rows_fused<true, N>), dim3((unsigned)blocks), dim3(256), 0, st, \
-                               idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
-    else hipLaunchKernelGGL((afm_rows_fused<false, N>), dim3((unsigned)blocks), dim3(256), 0, st, \
-                            idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);   \
+    if (tb) {                                                                              \
+      allow_lds((const void*)afm_rows_fused<true, N>, lds);                                 \
+      hipLaunchKernelGGL((afm_rows_fused<true, N>), dim3((unsigned)blocks), dim3(256), lds, st, \
+                         idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
+    } else {                                                                               \
+      allow_lds((const void*)afm_rows_fused<false, N>, lds);                                \
+      hipLaunchKernelGGL((afm_rows_fused<false, N>), dim3((unsigned)blocks), dim3(256), lds, st, \
+                         idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
+    }                                                                                      \
     return (int)hipGetLastError();                                                         \
   }
       HHFM_AFM_FUSED(1)
@@ -643,14 +677,17 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
       const size_t lds = afm_cat_fused_lds(F, k, A);
 #define HHFM_AFM_CAT_FUSED(N)                                                               \
   if (NT == N) {                                                                           \
-    if (tb)                                                                                \
+    if (tb) {                                                                              \
+      allow_lds((const void*)afm_cat_fused<true, N>, lds);                                  \
       hipLaunchKernelGGL((afm_cat_fused<true, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, F, \
                          E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                   \
                          (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
-    else                                                                                   \
+    } else {                                                                               \
+      allow_lds((const void*)afm_cat_fused<false, N>, lds);                                 \
       hipLaunchKernelGGL((afm_cat_fused<false, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, \
                          F, E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                \
                          (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
+    }                                                                                      \
   }
       HHFM_AFM_CAT_FUSED(1)
       HHFM_AFM_CAT_FUSED(2)

@@ -117,7 +117,7 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     (4, 16, 8, "bf16", 70, 64, 5),        # fused: one tile pair per query group
     (9, 32, 32, "f32", 11, 500, 20),      # GEMM path: 8 query fields
     (5, 20, 16, "f32", 13, 400, 20),      # GEMM path: k % 8 != 0
-    (5, 128, 128, "f32", 6, 300, 20),     # GEMM path: Wᵀ image > 64 KB of LDS
+    (5, 128, 128, "f32", 6, 300, 20),     # fused: 75 KB of LDS (raised dynamic limit)
 ])
 def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
     """A2 across the fused kernel's envelope and the GEMM path beyond it."""
