@@ -100,7 +100,7 @@ static void allow_lds(const void* fn, size_t bytes) {
 }
 static size_t afm_rows_fused_lds(int k, int A) {
   const int NA = (A + 31) / 32 * 32;
-  return 4 * (size_t)(NA * k + k + 2 * NA);
+  return 4 * (size_t)(NA * k + k + 2 * NA + 4 * 32 * 4);   // + 4 waves x 32 combos x float4
 }
 
 template <bool TBF, int NT>
@@ -221,30 +221,43 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
 #pragma unroll
     for (int n = 0; n < NT; ++n)
 #pragma unroll
-      for (int x = 0; x < 16; ++x) {
-        const int u = 32 * n + 8 * (x >> 2) + 4 * h + (x & 3);
-        lg = fmaf(fmaxf(acc[n][x] + bl[u], 0.f), apl[u], lg);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int u = 32 * n + 8 * g4 + 4 * h;
+        const float4 bq = *reinterpret_cast<const float4*>(bl + u);
+        const float4 pq = *reinterpret_cast<const float4*>(apl + u);
+        lg = fmaf(fmaxf(acc[n][4 * g4 + 0] + bq.x, 0.f), pq.x, lg);
+        lg = fmaf(fmaxf(acc[n][4 * g4 + 1] + bq.y, 0.f), pq.y, lg);
+        lg = fmaf(fmaxf(acc[n][4 * g4 + 2] + bq.z, 0.f), pq.z, lg);
+        lg = fmaf(fmaxf(acc[n][4 * g4 + 3] + bq.w, 0.f), pq.w, lg);
       }
     lg += __shfl_xor(lg, 32, kWave);
     sP += __shfl_xor(sP, 32, kWave);
     // softmax over the row's np pairs (tf.nn.softmax, AFM.py:125) and the
-    // attention-weighted sum of the pair scores
-    const int base = (live ? r : 0) * np;
-    float mx = kNegInf;
-    for (int q = 0; q < np; ++q) mx = fmaxf(mx, __shfl(lg, base + q, kWave));
-    float se = 0.f, num = 0.f;
-    for (int q = 0; q < np; ++q) {
-      const float ee = expf(__shfl(lg, base + q, kWave) - mx);
-      se += ee;
-      num = fmaf(ee, __shfl(sP, base + q, kWave), num);
+    // attention-weighted sum of the pair scores, by the row's first lane from
+    // the combos' (logit, pair score, Σw share) parked in LDS — independent
+    // reads instead of a serial chain of cross-lane shuffles.  (One wave's LDS
+    // accesses complete in order, so no barrier.)
+    float4* ep = reinterpret_cast<float4*>(apl + NA) + 32 * wv;
+    if (h == 0) ep[j] = make_float4(lg, sP, wf, 0.f);
+    if (ok && p == 0 && h == 0) {
+      const float4* e = ep + r * np;
+      float mx = kNegInf;
+      for (int q = 0; q < np; ++q) mx = fmaxf(mx, e[q].x);
+      float se = 0.f, num = 0.f;
+      for (int q = 0; q < np; ++q) {
+        const float4 eq = e[q];
+        const float ee = expf(eq.x - mx);
+        se += ee;
+        num = fmaf(ee, eq.y, num);
+      }
+      float fb = 0.f;
+      if (np >= F) {   // the row's lanes fetched one field each
+        for (int f = 0; f < F; ++f) fb += e[f].z;
+      } else {         // F = 2: one lane per row
+        for (int f = 0; f < F; ++f) fb += w[clamp_id(idx[row * F + f], M)];
+      }
+      out[row] = (num / se + fb) + w0;   // add_n, AFM.py:142
     }
-    float fb = 0.f;
-    if (np >= F) {   // the row's lanes fetched one field each
-      for (int f = 0; f < F; ++f) fb += __shfl(wf, base + f, kWave);
-    } else {         // F = 2: one lane per row
-      for (int f = 0; f < F; ++f) fb += ok ? w[clamp_id(idx[row * F + f], M)] : 0.f;
-    }
-    if (ok && p == 0 && h == 0) out[row] = (num / se + fb) + w0;   // add_n, AFM.py:142
   }
 }
 
@@ -457,10 +470,16 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
 #pragma unroll
         for (int n = 0; n < NT; ++n)
 #pragma unroll
-          for (int x = 0; x < 16; ++x) {
-            const int u = 32 * n + 8 * (x >> 2) + 4 * h + (x & 3);
-            lg = fmaf(fmaxf(acc[n][x] + bl[u], 0.f), apl[u], lg);
-            acc[n][x] = 0.f;
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const int u = 32 * n + 8 * g4 + 4 * h;
+            const float4 bq = *reinterpret_cast<const float4*>(bl + u);
+            const float4 pq = *reinterpret_cast<const float4*>(apl + u);
+            const float bv[4] = {bq.x, bq.y, bq.z, bq.w}, pv[4] = {pq.x, pq.y, pq.z, pq.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              lg = fmaf(fmaxf(acc[n][4 * g4 + e] + bv[e], 0.f), pv[e], lg);
+              acc[n][4 * g4 + e] = 0.f;
+            }
           }
         lg += __shfl_xor(lg, 32, kWave);
         sP += __shfl_xor(sP, 32, kWave);
