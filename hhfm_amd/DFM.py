@@ -141,7 +141,9 @@ class DeepFM(ScoringModel):
         return super()._run_fetch(fetch, feed)
 
     def partial_fit(self, data):
-        raise NotImplementedError("DeepFM training (partial_fit) is not implemented yet")
+        """DFM.py:214-217 on the gfx950 train-step kernels (fp32)."""
+        from .training import dfm_partial_fit
+        return dfm_partial_fit(self, data)
 
 
 class Train(harness.Train):

@@ -270,6 +270,41 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_hhfm_train_step");
         });
 
+  m.def("dfm_train_workspace",
+        [](int64_t B, int F, int k, int64_t M, std::vector<int32_t> dims) {
+          size_t ws = 0;
+          check(hhfm_dfm_train_workspace(B, F, k, M, (int)dims.size(), dims.data(), &ws),
+                "hhfm_dfm_train_workspace");
+          return ws;
+        });
+
+  m.def("dfm_train_step",
+        [](uptr idx, uptr y, int64_t B, int F, uptr E, uptr w, int64_t M, int k,
+           std::vector<int32_t> dims, std::vector<uptr> W, std::vector<uptr> bias, uptr Wp,
+           uptr bp, float lr, float lam, int opt, std::vector<uptr> acc, uptr ws,
+           size_t ws_bytes, uptr loss, uptr stream) {
+          if (W.size() != dims.size() || bias.size() != dims.size())
+            throw py::value_error("dims, W and bias must have the same length");
+          if (opt == 0 && acc.size() != 2 * dims.size() + 4)
+            throw py::value_error("acc needs 2 * len(dims) + 4 accumulators");
+          std::vector<float*> Wv(W.size()), bv(bias.size()), av(acc.size());
+          for (size_t i = 0; i < W.size(); ++i) {
+            Wv[i] = P<float>(W[i]);
+            bv[i] = P<float>(bias[i]);
+          }
+          for (size_t i = 0; i < acc.size(); ++i) av[i] = P<float>(acc[i]);
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_dfm_train_step(P<const int32_t>(idx), P<const float>(y), B, F, P<float>(E),
+                                     P<float>(w), M, k, (int)dims.size(), dims.data(), Wv.data(),
+                                     bv.data(), P<float>(Wp), P<float>(bp), lr, lam, opt,
+                                     av.empty() ? nullptr : av.data(), P<void>(ws), ws_bytes,
+                                     P<float>(loss), P<void>(stream));
+          }
+          check(rc, "hhfm_dfm_train_step");
+        });
+
   m.def("topk_dense",
         [](uptr scores, int64_t B, int N, int64_t ld, int K, int base, uptr top_score,
            uptr top_idx, uptr stream) {

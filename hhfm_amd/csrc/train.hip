@@ -4,6 +4,8 @@
 //                         (Newcode/FM.py:123-136, 168-171)
 //   hhfm_hhfm_train_step  replaces the same for OUR
 //                         (Newcode/OurModel7.py:172-193, 219-228)
+//   hhfm_dfm_train_step   replaces the same for DeepFM
+//                         (Newcode/DFM.py:139-155, 214-217)
 //
 // One wave per batch row computes the forward score(s) and scatters the
 // gradient of the row's loss into dense fp32 gradient buffers with float
@@ -15,7 +17,7 @@
 // gradient descent, and accumulates Σ var² of the pre-update table for the
 // reported loss (TF evaluates `loss` and the update in the same run).
 // Gradients of reduce_max split equally between tied maxima (TF _MaxGrad).
-#include "hhfm_common.h"
+#include "gemm_mfma.h"
 
 namespace hhfm {
 
@@ -185,6 +187,249 @@ static int grid_for_n(int64_t n) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
+// ---------------------------------------------------------------------------
+// DeepFM training (fp32, the reference numerics).  Forward: the MLP as
+// exact-fp32 MFMA GEMMs (gemm_mfma.h, layer 0 gathering its A rows from the
+// table), activations kept for the backward pass.  Backward: a row kernel for
+// the concat projection (out, d = out − y, dWp, dbp, dw, the last layer's
+// delta), per layer dW = Hᵀ·G and G_prev = (G·Wᵀ) ⊙ relu' as GEMMs on
+// transposed / zero-padded copies, and a scatter of the embedding gradient
+// (deep part + FM part ∂y2/∂e_f = Σe − e_f).  Every activation row is padded
+// to a multiple of 8 floats and every transposed copy to Bp = pad8(B) columns,
+// zero-filled, so the GEMM's 16-byte K chunks never read past a row.
+// ---------------------------------------------------------------------------
+constexpr int kDfmTrainMaxLayers = 4;
+constexpr int kDfmHeadMaxCols = 1024;   // F + k + d_L per concat row
+
+static int64_t pad8(int64_t x) { return (x + 7) & ~int64_t(7); }
+
+// dst[c][r] = src[r][c] (r < R, c < C; zero for R <= r < Rp) and, with a mask
+// H, both the masked src (written back in place) and its transpose use
+// src ⊙ (H > 0).  32x32 tiles through LDS.
+__global__ __launch_bounds__(256) void tr_pad(float* __restrict__ src, int64_t R, int C,
+                                              int64_t lds, const float* __restrict__ H,
+                                              int64_t ldh, float* __restrict__ dst,
+                                              int64_t ldd, int64_t Rp) {
+  __shared__ float t[32][33];
+  const int64_t r0 = (int64_t)blockIdx.x * 32;
+  const int c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int64_t r = r0 + i;
+    const int c = c0 + tx;
+    float v = 0.f;
+    if (r < R && c < C) {
+      v = src[r * lds + c];
+      if (H) {
+        v = H[r * ldh + c] > 0.f ? v : 0.f;
+        src[r * lds + c] = v;
+      }
+    }
+    t[i][tx] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i;
+    const int64_t r = r0 + tx;
+    if (c < C && r < Rp) dst[c * ldd + r] = t[tx][i];
+  }
+}
+
+// dst[r][c] = src[r][c] for c < C, 0 for C <= c < ldd (row-major zero pad)
+__global__ __launch_bounds__(256) void copy_pad(const float* __restrict__ src, int64_t R, int C,
+                                                float* __restrict__ dst, int ldd) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R * ldd;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / ldd;
+    const int c = (int)(i - r * ldd);
+    dst[i] = c < C ? src[r * C + c] : 0.f;
+  }
+}
+
+// X0ᵀ[c][m] = E[x_m, c/k][c%k] (m < B), 0 for B <= m < Bp
+__global__ __launch_bounds__(256) void gather_tr(const int32_t* __restrict__ idx, int64_t B,
+                                                 int F, const float* __restrict__ E, int64_t M,
+                                                 int k, float* __restrict__ dst, int64_t Bp) {
+  __shared__ float t[32][33];
+  const int64_t m0 = (int64_t)blockIdx.x * 32;
+  const int c0 = blockIdx.y * 32;
+  const int D = F * k;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int i = ty; i < 32; i += 8) {
+    const int64_t m = m0 + i;
+    const int c = c0 + tx;
+    float v = 0.f;
+    if (m < B && c < D) {
+      const int f = c / k;
+      v = E[(int64_t)clamp_id(idx[m * F + f], M) * k + (c - f * k)];
+    }
+    t[i][tx] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i;
+    const int64_t m = m0 + tx;
+    if (c < D && m < Bp) dst[c * Bp + m] = t[tx][i];
+  }
+}
+
+// db[n] = Σ_m G_T[n][m]  (wave per output)
+__global__ __launch_bounds__(256) void row_sums(const float* __restrict__ GT, int N, int64_t ld,
+                                                int64_t cols, float* __restrict__ out) {
+  const int l = threadIdx.x & 63;
+  const int64_t n = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int64_t m = l; m < cols; m += kWave) s += GT[n * ld + m];
+  s = group_sum<kWave>(s);
+  if (l == 0) out[n] = s;
+}
+
+// Concat projection, forward and backward (DFM.py:109-137, l2_loss), wave
+// per row; each lane keeps its columns' dWp partials over the block's rows.
+// scal[0] += dbp  scal[1] += (out − y)²/2
+__global__ __launch_bounds__(256) void dfm_train_head(
+    const int32_t* __restrict__ idx, const float* __restrict__ y, int64_t B, int F,
+    const float* __restrict__ E, const float* __restrict__ w, int64_t M, int k,
+    const float* __restrict__ HL, int dL, int64_t ldh, const float* __restrict__ Wp,
+    const float* __restrict__ bp, float* __restrict__ GL, float* __restrict__ gvec,
+    float* __restrict__ dWp, float* __restrict__ dw, float* __restrict__ scal) {
+  constexpr int NJ = kDfmHeadMaxCols / kWave;
+  const int l = threadIdx.x & 63;
+  const int D = F + k + dL;
+  float part[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) part[j] = 0.f;
+  float sb = 0.f, sl = 0.f;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* x = idx + m * F;
+    // this lane's concat columns c = l + 64 j: [y1 (F) | y2 (k) | h_L (dL)]
+    float cv[NJ];
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = l + kWave * j;
+      float v = 0.f;
+      if (c < F) {
+        v = w[clamp_id(x[c], M)];
+      } else if (c < F + k) {
+        const int cc = c - F;
+        float s = 0.f, q = 0.f;
+        for (int f = 0; f < F; ++f) {
+          const float e = E[(int64_t)clamp_id(x[f], M) * k + cc];
+          s += e;
+          q += e * e;
+        }
+        v = 0.5f * (s * s - q);
+      } else if (c < D) {
+        v = HL[m * ldh + (c - F - k)];
+      }
+      cv[j] = v;
+      if (c < D) dot = fmaf(v, Wp[c], dot);
+    }
+    const float out = group_sum<kWave>(dot) + bp[0];
+    const float g = out - y[m];                    // d l2_loss(y − out) / d out
+    sb += g;
+    sl += 0.5f * g * g;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = l + kWave * j;
+      if (c < D) part[j] = fmaf(g, cv[j], part[j]);
+      if (c < F) atomicAdd(&dw[clamp_id(x[c], M)], g * Wp[c]);
+      if (c >= F + k && c < D) {
+        const int n = c - F - k;
+        GL[m * ldh + n] = cv[j] > 0.f ? g * Wp[c] : 0.f;   // relu' of the last layer
+      }
+    }
+    if (l == 0) gvec[m] = g;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = l + kWave * j;
+    if (c < D && part[j] != 0.f) atomicAdd(&dWp[c], part[j]);
+  }
+  if (l == 0) {   // (g is wave-uniform: every lane holds the same sums)
+    atomicAdd(&scal[0], sb);
+    atomicAdd(&scal[1], sl);
+  }
+}
+
+// dE[x_f][c] += dX0[m][f·k + c] + g_m·Wp[F+c]·(Σ_f' e_f'c − e_fc)   (wave per row)
+__global__ __launch_bounds__(256) void dfm_train_scatter(
+    const int32_t* __restrict__ idx, int64_t B, int F, const float* __restrict__ E, int64_t M,
+    int k, const float* __restrict__ dX0, const float* __restrict__ gvec,
+    const float* __restrict__ Wp, float* __restrict__ dE) {
+  const int l = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* x = idx + m * F;
+    const float g = gvec[m];
+    for (int c = l; c < k; c += kWave) {
+      float s = 0.f;
+      for (int f = 0; f < F; ++f) s += E[(int64_t)clamp_id(x[f], M) * k + c];
+      const float gy2 = g * Wp[F + c];
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = clamp_id(x[f], M);
+        const float e = E[id * k + c];
+        atomicAdd(&dE[id * k + c], dX0[m * (int64_t)(F * k) + f * k + c] + gy2 * (s - e));
+      }
+    }
+  }
+}
+
+struct DfmTrainPlan {
+  int64_t Bp;
+  int L, D0;
+  int d[kDfmTrainMaxLayers + 1];     // d[0] = F·k, d[l+1] = layer l width
+  int64_t off_WtP[kDfmTrainMaxLayers], off_WP[kDfmTrainMaxLayers];
+  int64_t off_dW[kDfmTrainMaxLayers], off_db[kDfmTrainMaxLayers];
+  int64_t off_H[kDfmTrainMaxLayers + 1], off_HT[kDfmTrainMaxLayers];
+  int64_t off_G[kDfmTrainMaxLayers + 1], off_GT[kDfmTrainMaxLayers + 1];
+  int64_t off_dX0, off_g, off_dWp, off_dE, off_dw, off_scal;
+  int64_t total;   // floats
+};
+
+static bool dfm_train_plan(int64_t B, int F, int k, int64_t M, int L, const int32_t* dims,
+                           DfmTrainPlan& p) {
+  if (L < 1 || L > kDfmTrainMaxLayers || F < 1 || k < 4 || k % 4) return false;
+  p = DfmTrainPlan{};
+  p.L = L;
+  p.D0 = F * k;
+  p.d[0] = p.D0;
+  for (int i = 0; i < L; ++i) {
+    if (dims[i] < 1) return false;
+    p.d[i + 1] = dims[i];
+  }
+  if (F + k + p.d[L] > kDfmHeadMaxCols) return false;
+  p.Bp = pad8(B > 0 ? B : 1);
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  for (int i = 0; i < L; ++i) {
+    p.off_WtP[i] = take((int64_t)p.d[i + 1] * pad8(p.d[i]));
+    p.off_WP[i] = take((int64_t)p.d[i] * pad8(p.d[i + 1]));
+    p.off_dW[i] = take((int64_t)p.d[i] * p.d[i + 1]);
+    p.off_db[i] = take(p.d[i + 1]);
+    p.off_HT[i] = take((int64_t)p.d[i] * p.Bp);
+  }
+  for (int i = 1; i <= L; ++i) {
+    p.off_H[i] = take(p.Bp * pad8(p.d[i]));
+    p.off_G[i] = take(p.Bp * pad8(p.d[i]));
+    p.off_GT[i] = take((int64_t)p.d[i] * p.Bp);
+  }
+  p.off_dX0 = take(p.Bp * p.D0);
+  p.off_g = take(p.Bp);
+  p.off_dWp = take(F + k + p.d[L]);
+  // zero-initialised, kept zeroed by the step: dE, dw, scalars
+  p.off_dE = take(M * k);
+  p.off_dw = take(M);
+  p.off_scal = take(16);
+  p.total = o;
+  return true;
+}
+
 }  // namespace hhfm
 
 using namespace hhfm;
@@ -244,5 +489,164 @@ extern "C" int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_
   hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, dE, accE, nE,
                      lr, lam, optimizer, scal + 2);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lam, loss);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_dfm_train_workspace(int64_t B, int32_t F, int32_t k, int64_t features_M,
+                                        int32_t nlayers, const int32_t* layer_dims,
+                                        size_t* ws_bytes) {
+  DfmTrainPlan p;
+  if (!ws_bytes || !layer_dims || B < 0 || features_M < 1 ||
+      !dfm_train_plan(B, F, k, features_M, nlayers, layer_dims, p))
+    return HHFM_EINVAL;
+  *ws_bytes = (size_t)p.total * 4;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F,
+                                   float* E, float* w, int64_t features_M, int32_t k,
+                                   int32_t nlayers, const int32_t* layer_dims, float* const* W,
+                                   float* const* bias, float* Wp, float* bp, float lr,
+                                   float lambda_l2, int32_t optimizer, float* const* acc,
+                                   void* workspace, size_t ws_bytes, float* loss,
+                                   void* stream) {
+  DfmTrainPlan p;
+  if (B < 0 || features_M < 1 || !layer_dims ||
+      !dfm_train_plan(B, F, k, features_M, nlayers, layer_dims, p))
+    return HHFM_EINVAL;
+  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!idx || !y || !E || !w || !W || !bias || !Wp || !bp || !loss || !workspace)
+    return HHFM_EINVAL;
+  const int L = p.L;
+  for (int i = 0; i < L; ++i)
+    if (!W[i] || !bias[i]) return HHFM_EINVAL;
+  if (optimizer == OPT_ADAGRAD) {   // acc: E, w, W_0..W_{L-1}, b_0..b_{L-1}, Wp, bp
+    if (!acc) return HHFM_EINVAL;
+    for (int i = 0; i < 2 * L + 4; ++i)
+      if (!acc[i]) return HHFM_EINVAL;
+  }
+  if (ws_bytes < (size_t)p.total * 4) return HHFM_EWORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  auto at = [&](int64_t off) { return ws + off; };
+  float* scal = at(p.off_scal);
+  const int64_t Bp = p.Bp;
+  const int64_t nE = features_M * k;
+  auto acc_of = [&](int i) { return optimizer == OPT_ADAGRAD ? acc[i] : (float*)nullptr; };
+
+  if (B > 0) {
+    // weights: Wᵀ zero-padded (forward Bt) and W zero-padded (backward Bt)
+    for (int i = 0; i < L; ++i) {
+      const int din = p.d[i], dout = p.d[i + 1];
+      hipLaunchKernelGGL(tr_pad, dim3((unsigned)((din + 31) / 32), (unsigned)((dout + 31) / 32)),
+                         dim3(256), 0, st, W[i], (int64_t)din, dout, (int64_t)dout,
+                         (const float*)nullptr, (int64_t)0, at(p.off_WtP[i]), pad8(din),
+                         pad8(din));
+      hipLaunchKernelGGL(copy_pad, dim3(grid_for_n((int64_t)din * pad8(dout))), dim3(256), 0, st,
+                         W[i], (int64_t)din, dout, at(p.off_WP[i]), (int)pad8(dout));
+    }
+    // forward: H_{i+1} = relu(H_i · W_i + b_i), H_0 gathered from the table
+    for (int i = 0; i < L; ++i) {
+      GemmArgs g{};
+      g.M = B;
+      g.N = p.d[i + 1];
+      g.K = p.d[i];
+      if (i == 0) {
+        g.gidx = idx;
+        g.T = E;
+        g.Mtab = features_M;
+        g.F = F;
+        g.kf = k;
+      } else {
+        g.A = at(p.off_H[i]);
+        g.lda = pad8(p.d[i]);
+      }
+      g.Bt = at(p.off_WtP[i]);
+      g.ldb = pad8(p.d[i]);
+      g.bias = bias[i];
+      g.relu = 1;
+      g.C = at(p.off_H[i + 1]);
+      g.ldc = pad8(p.d[i + 1]);
+      launch_gemm(g, false, 0, st);
+    }
+    // head: out, d = out − y, dWp, dbp, dw, last layer's delta
+    const int64_t ldL = pad8(p.d[L]);
+    (void)hipMemsetAsync(at(p.off_G[L]), 0, (size_t)(B * ldL) * 4, st);
+    hipLaunchKernelGGL(dfm_train_head, dim3(grid_for_n(B * 64 / 8)), dim3(256), 0, st, idx, y, B,
+                       F, E, w, features_M, k, at(p.off_H[L]), p.d[L], ldL, Wp, bp, at(p.off_G[L]),
+                       at(p.off_g), at(p.off_dWp), at(p.off_dw), scal);
+    hipLaunchKernelGGL(tr_pad, dim3((unsigned)((Bp + 31) / 32), (unsigned)((p.d[L] + 31) / 32)),
+                       dim3(256), 0, st, at(p.off_G[L]), B, p.d[L], ldL, (const float*)nullptr,
+                       (int64_t)0, at(p.off_GT[L]), Bp, Bp);
+    // backward through the layers
+    for (int i = L - 1; i >= 0; --i) {
+      const int din = p.d[i], dout = p.d[i + 1];
+      // H_iᵀ (transposed activations; the gathered table rows for i = 0)
+      if (i == 0)
+        hipLaunchKernelGGL(gather_tr, dim3((unsigned)((Bp + 31) / 32), (unsigned)((din + 31) / 32)),
+                           dim3(256), 0, st, idx, B, F, E, features_M, k, at(p.off_HT[0]), Bp);
+      else
+        hipLaunchKernelGGL(tr_pad, dim3((unsigned)((Bp + 31) / 32), (unsigned)((din + 31) / 32)),
+                           dim3(256), 0, st, at(p.off_H[i]), B, din, pad8(din),
+                           (const float*)nullptr, (int64_t)0, at(p.off_HT[i]), Bp, Bp);
+      {   // dW_i = H_iᵀ · G_{i+1}
+        GemmArgs g{};
+        g.M = din;
+        g.N = dout;
+        g.K = (int)Bp;
+        g.A = at(p.off_HT[i]);
+        g.lda = Bp;
+        g.Bt = at(p.off_GT[i + 1]);
+        g.ldb = Bp;
+        g.C = at(p.off_dW[i]);
+        g.ldc = dout;
+        launch_gemm(g, false, 0, st);
+      }
+      hipLaunchKernelGGL(row_sums, dim3((unsigned)((dout + 3) / 4)), dim3(256), 0, st,
+                         at(p.off_GT[i + 1]), dout, Bp, Bp, at(p.off_db[i]));
+      {   // G_i = (G_{i+1} · W_iᵀ) ⊙ relu'(H_i), or dX0 = G_1 · W_0ᵀ
+        GemmArgs g{};
+        g.M = B;
+        g.N = din;
+        g.K = dout;
+        g.A = at(p.off_G[i + 1]);
+        g.lda = pad8(dout);
+        g.Bt = at(p.off_WP[i]);
+        g.ldb = pad8(dout);
+        g.C = i == 0 ? at(p.off_dX0) : at(p.off_G[i]);
+        g.ldc = i == 0 ? p.D0 : pad8(din);
+        launch_gemm(g, false, 0, st);
+      }
+      if (i > 0)
+        hipLaunchKernelGGL(tr_pad, dim3((unsigned)((Bp + 31) / 32), (unsigned)((din + 31) / 32)),
+                           dim3(256), 0, st, at(p.off_G[i]), B, din, pad8(din),
+                           (const float*)at(p.off_H[i]), pad8(din), at(p.off_GT[i]), Bp, Bp);
+    }
+    hipLaunchKernelGGL(dfm_train_scatter, dim3(grid_for_n(B * 64)), dim3(256), 0, st, idx, B, F,
+                       E, features_M, k, at(p.off_dX0), at(p.off_g), Wp, at(p.off_dE));
+  }
+  // optimizer: λ only on the layer weights and the concat projection (DFM.py:146-152)
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, at(p.off_dE),
+                     acc_of(0), nE, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(features_M)), dim3(256), 0, st, w,
+                     at(p.off_dw), acc_of(1), features_M, lr, 0.f, optimizer, (float*)nullptr);
+  for (int i = 0; i < L; ++i) {
+    const int64_t n = (int64_t)p.d[i] * p.d[i + 1];
+    if (B == 0) {
+      (void)hipMemsetAsync(at(p.off_dW[i]), 0, n * 4, st);
+      (void)hipMemsetAsync(at(p.off_db[i]), 0, p.d[i + 1] * 4, st);
+    }
+    hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(n)), dim3(256), 0, st, W[i],
+                       at(p.off_dW[i]), acc_of(2 + i), n, lr, lambda_l2, optimizer, scal + 2);
+    hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(p.d[i + 1])), dim3(256), 0, st, bias[i],
+                       at(p.off_db[i]), acc_of(2 + L + i), (int64_t)p.d[i + 1], lr, 0.f,
+                       optimizer, (float*)nullptr);
+  }
+  const int64_t nWp = F + k + p.d[L];
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nWp)), dim3(256), 0, st, Wp, at(p.off_dWp),
+                     acc_of(2 + 2 * L), nWp, lr, lambda_l2, optimizer, scal + 2);
+  hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, bp, acc_of(3 + 2 * L), scal, lr,
+                     optimizer);
+  hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lambda_l2, loss);
   return (int)hipGetLastError();
 }

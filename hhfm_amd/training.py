@@ -94,6 +94,43 @@ def hhfm_partial_fit(model, data) -> float:
     return float(st["loss"].item())
 
 
+def dfm_partial_fit(model, data) -> float:
+    """DeepFM.partial_fit (DFM.py:214-217): one TF Adagrad step on every
+    variable (DFM.py:155), loss l2_loss(y − out) + l2_reg on the concat
+    projection and the layer weights (DFM.py:143-152)."""
+    W = model.weights
+    L = len(model.deep_layers)
+    names = (["feature_embeddings", "feature_bias"] + [f"layer_{i}" for i in range(L)]
+             + [f"bias_{i}" for i in range(L)] + ["concat_projection", "concat_bias"])
+    st = getattr(model, "_train_state", None)
+    if st is None:
+        if model.table_dtype != torch.float32:
+            raise NotImplementedError("training runs on fp32 tables")
+        st = {n: torch.full_like(W[n], 0.1) for n in names}
+        st["loss"] = torch.zeros(1, dtype=torch.float32, device=model.device)
+        st["ws"], st["ws_rows"] = None, 0
+        model._train_state = st
+    X = model._idx(data["X"])
+    y = torch.as_tensor(np.asarray(data["Y"], np.float32).reshape(-1)).to(model.device)
+    B, F = X.shape
+    M, k = W["feature_embeddings"].shape
+    dims = [int(d) for d in model.deep_layers]
+    nat = native()
+    if st["ws"] is None or st["ws_rows"] < B:
+        nbytes = nat.dfm_train_workspace(B, F, k, M, dims)
+        st["ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=model.device)
+        st["ws_rows"] = B
+    ptr = lambda n: W[n].data_ptr()  # noqa: E731
+    nat.dfm_train_step(X.data_ptr(), y.data_ptr(), B, F, ptr("feature_embeddings"),
+                       ptr("feature_bias"), M, k, dims, [ptr(f"layer_{i}") for i in range(L)],
+                       [ptr(f"bias_{i}") for i in range(L)], ptr("concat_projection"),
+                       ptr("concat_bias"), float(model.learning_rate), float(model.l2_reg), 0,
+                       [st[n].data_ptr() for n in names], st["ws"].data_ptr(), st["ws"].numel(),
+                       st["loss"].data_ptr(), ops._stream(model.device))
+    model._prep = None   # the scoring path's prepared (transposed / bf16) weights are stale
+    return float(st["loss"].item())
+
+
 def _log(tr, line):
     print(line)
     path = getattr(tr.args, "result_file", None)

@@ -222,6 +222,25 @@ int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_t B, int32_
                          int32_t k, float lr, float lambda_l2, int32_t optimizer, float* accE,
                          void* workspace, size_t ws_bytes, float* loss, void* stream);
 
+/* DeepFM (DFM.py:139-155, 214-217; use_fm = use_deep = True, loss "mse"):
+ *   loss = Σ (y − out)²/2 + λ·(‖Wp‖² + Σ_l ‖W_l‖²)/2
+ * one step of TF Adagrad (optimizer 0) or gradient descent (1) on every
+ * variable, in place.  W[l] is layer l row-major [d_{l-1}][d_l] (d_{-1} =
+ * F·k), bias[l] [d_l], Wp the concat projection [F + k + d_{L-1}], bp a
+ * device float.  acc (Adagrad): 2L+4 device accumulators in the order E, w,
+ * W_0..W_{L-1}, b_0..b_{L-1}, Wp, bp, initialised to 0.1 by the caller.
+ * The workspace (hhfm_dfm_train_workspace bytes for batches of at most B rows)
+ * must be zero-filled once; the step keeps its gradient regions zeroed.
+ * Requires k % 4 == 0, L <= 4, F + k + d_{L-1} <= 1024. */
+int hhfm_dfm_train_workspace(int64_t B, int32_t F, int32_t k, int64_t features_M,
+                             int32_t nlayers, const int32_t* layer_dims, size_t* ws_bytes);
+int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F, float* E,
+                        float* w, int64_t features_M, int32_t k, int32_t nlayers,
+                        const int32_t* layer_dims, float* const* W, float* const* bias,
+                        float* Wp, float* bp, float lr, float lambda_l2, int32_t optimizer,
+                        float* const* acc, void* workspace, size_t ws_bytes, float* loss,
+                        void* stream);
+
 /* tf.nn.top_k(scores, K) over a materialised score matrix [B][ld] (first N
  * columns), K <= 64; ids reported as global_item_base + column. */
 int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,

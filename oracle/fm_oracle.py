@@ -350,3 +350,66 @@ def hhfm_train_step(X, Neg, E, accE, lr, lam, feature_dimension, time_dimension,
     else:
         E = E - F32(lr) * dE
     return loss, E, accE
+
+
+def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="adagrad"):
+    """DeepFM partial_fit (DFM.py:139-155, 214-217), use_fm = use_deep = True,
+    loss_type "mse": loss = l2_loss(y − out) + λ·(‖Wp‖² + Σ_l ‖W_l‖²)/2
+    (l2_regularizer on concat_projection and every layer_i; not on the
+    embeddings, biases or concat_bias), one TF Adagrad step on every variable.
+    acc: dict of accumulators keyed E, w, W0.., b0.., Wp, bp (updated copies
+    are returned).  Returns (loss, E, w, layers, biases, Wp, bp, acc)."""
+    X = np.asarray(X, np.int64)
+    y = np.asarray(y, F32).reshape(-1)
+    E = np.asarray(E, F32)
+    w = np.asarray(w, F32).reshape(-1)
+    layers = [np.asarray(W, F32) for W in layers]
+    biases = [np.asarray(b, F32).reshape(-1) for b in biases]
+    Wp = np.asarray(Wp, F32).reshape(-1)
+    B, F = X.shape
+    k = E.shape[1]
+    e = E[X]                                                          # :104
+    y1 = w[X]                                                         # :109-110
+    s = e.sum(1, dtype=F32)
+    y2 = F32(0.5) * (s * s - (e * e).sum(1, dtype=F32))               # :114-122
+    hs = [e.reshape(B, F * k)]
+    for W, b in zip(layers, biases):                                  # :125-128
+        hs.append(np.maximum(np.matmul(hs[-1], W).astype(F32) + b, 0).astype(F32))
+    cat = np.concatenate([y1, y2, hs[-1]], axis=1)                    # :132
+    out = np.matmul(cat, Wp).astype(F32) + F32(bp)                    # :137
+    r = y - out
+    reg = np.sum(Wp.astype(np.float64) ** 2) + sum(np.sum(W.astype(np.float64) ** 2)
+                                                     for W in layers)
+    loss = F32(np.sum(r.astype(np.float64) ** 2) / 2 + lam * reg / 2)  # :143, :146-152
+    g = -r                                                            # d loss / d out
+    dWp = np.matmul(cat.T, g).astype(F32) + F32(lam) * Wp
+    dbp = F32(g.sum(dtype=np.float64))
+    dcat = g[:, None] * Wp[None, :]
+    dh = dcat[:, F + k:]
+    dWs, dbs = [None] * len(layers), [None] * len(layers)
+    for i in range(len(layers) - 1, -1, -1):
+        dz = (dh * (hs[i + 1] > 0)).astype(F32)                       # relu'
+        dWs[i] = np.matmul(hs[i].T, dz).astype(F32) + F32(lam) * layers[i]
+        dbs[i] = dz.sum(0, dtype=F32)
+        dh = np.matmul(dz, layers[i].T).astype(F32)
+    de = dh.reshape(B, F, k) + dcat[:, None, F:F + k] * (s[:, None, :] - e)
+    dE = np.zeros_like(E)
+    dw = np.zeros_like(w)
+    for f in range(F):
+        np.add.at(dE, X[:, f], de[:, f])
+        np.add.at(dw, X[:, f], dcat[:, f])
+    acc = {key: np.asarray(v, F32).copy() for key, v in acc.items()}
+
+    def upd(var, grad, key):
+        if optimizer == "adagrad":
+            var, acc[key] = tf_adagrad(var, grad, acc[key], lr)
+            return var
+        return (var - F32(lr) * grad).astype(F32)
+
+    E = upd(E, dE, "E")
+    w = upd(w, dw, "w")
+    layers = [upd(W, dW, f"W{i}") for i, (W, dW) in enumerate(zip(layers, dWs))]
+    biases = [upd(b, db, f"b{i}") for i, (b, db) in enumerate(zip(biases, dbs))]
+    Wp = upd(Wp, dWp, "Wp")
+    bp = upd(np.float32(bp), dbp, "bp")
+    return loss, E, w, layers, biases, Wp, F32(bp), acc

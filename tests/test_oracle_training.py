@@ -66,6 +66,54 @@ def test_hhfm_gradient_matches_finite_differences():
     assert np.allclose(got, fd, rtol=3e-3, atol=3e-4)
 
 
+def test_dfm_gradient_matches_finite_differences():
+    """DeepFM (DFM.py:139-155): every variable's gradient, incl. a repeated id."""
+    rng = np.random.default_rng(2)
+    M, k, B, F, lam = 30, 4, 16, 3, 0.05
+    X = rng.integers(0, M, (B, F))
+    X[0, 1] = X[0, 0]
+    y = rng.choice([1.0, -1.0], B)
+    E, w = rng.normal(0, 0.3, (M, k)), rng.normal(0, 0.3, M)
+    Ls = [rng.normal(0, 0.5, (F * k, 6)), rng.normal(0, 0.5, (6, 5))]
+    bs = [rng.normal(0, 0.3, 6), rng.normal(0.3, 0.1, 5)]
+    Wp, bp = rng.normal(0, 0.5, F + k + 5), 0.01
+
+    def loss(E, w, Ls, bs, Wp, bp):
+        e = E[X]
+        s = e.sum(1)
+        h = e.reshape(B, -1)
+        for W, b in zip(Ls, bs):
+            h = np.maximum(h @ W + b, 0)
+        out = np.concatenate([w[X], 0.5 * (s * s - (e * e).sum(1)), h], 1) @ Wp + bp
+        return ((y - out) ** 2).sum() / 2 + lam * ((Wp ** 2).sum() + sum((W ** 2).sum() for W in Ls)) / 2
+
+    lr = 1e-3
+    l0, E1, w1, L1, b1, Wp1, bp1, _ = orc.dfm_train_step(X, y, E, w, Ls, bs, Wp, bp, {}, lr, lam,
+                                                          optimizer="sgd")
+    assert abs(l0 - loss(E, w, Ls, bs, Wp, bp)) < 1e-4 * abs(l0)
+
+    def fd(fn, arr, i, eps=1e-5):
+        a = arr.copy()
+        a[i] += eps
+        lp = fn(a)
+        a[i] -= 2 * eps
+        return (lp - fn(a)) / (2 * eps)
+
+    checks = [
+        ((E.astype(np.float32) - E1) / lr, (X[0, 0], 1), fd(lambda a: loss(a, w, Ls, bs, Wp, bp), E, (X[0, 0], 1))),
+        ((w.astype(np.float32) - w1) / lr, (X[2, 1],), fd(lambda a: loss(E, a, Ls, bs, Wp, bp), w, (X[2, 1],))),
+        ((Ls[0].astype(np.float32) - L1[0]) / lr, (3, 2), fd(lambda a: loss(E, w, [a, Ls[1]], bs, Wp, bp), Ls[0], (3, 2))),
+        ((Ls[1].astype(np.float32) - L1[1]) / lr, (1, 4), fd(lambda a: loss(E, w, [Ls[0], a], bs, Wp, bp), Ls[1], (1, 4))),
+        ((bs[1].astype(np.float32) - b1[1]) / lr, (2,), fd(lambda a: loss(E, w, Ls, [bs[0], a], Wp, bp), bs[1], (2,))),
+        ((Wp.astype(np.float32) - Wp1) / lr, (F + k + 2,), fd(lambda a: loss(E, w, Ls, bs, a, bp), Wp, (F + k + 2,))),
+        ((Wp.astype(np.float32) - Wp1) / lr, (F + 1,), fd(lambda a: loss(E, w, Ls, bs, a, bp), Wp, (F + 1,))),
+    ]
+    for grad, i, ref in checks:
+        assert np.isclose(grad[i], ref, rtol=2e-3, atol=2e-4), (i, grad[i], ref)
+    dbp = (np.float32(bp) - bp1) / lr
+    assert np.isclose(dbp, fd(lambda a: loss(E, w, Ls, bs, Wp, a[0]), np.array([bp]), (0,)), rtol=2e-3)
+
+
 def test_tf_adagrad_semantics():
     v, g, a = np.float32([1.0]), np.float32([0.5]), np.float32([0.1])
     v1, a1 = orc.tf_adagrad(v, g, a, 0.1)
