@@ -162,13 +162,25 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     uint4 v[TBF ? 4 : 8];
   };
   const int myrow = 32 * wv + r;
-  auto eload = [&](EChunk& e, int c) {
+  // layer-0 step cursor (step S: field f = S % F, columns col = 16·(S / F)),
+  // advanced incrementally: wave-uniform, so it lives in SGPRs without a
+  // division per step
+  struct Cur {
+    int S, f, col;
+  };
+  auto adv = [&](Cur& u) {
+    ++u.S;
+    if (++u.f == F) {
+      u.f = 0;
+      u.col += 16;
+    }
+  };
+  auto eload = [&](EChunk& e, Cur& u) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int S = 4 * c + s;
-      const bool real = S < nS;                  // padding steps: zero weights
-      const int64_t id = ids[myrow * F + (real ? S % F : 0)];
-      const int col = (real ? 16 * (S / F) : 0) + 8 * h;
+      const bool real = u.S < nS;                // padding steps: zero weights
+      const int64_t id = ids[myrow * F + (real ? u.f : 0)];
+      const int col = (real ? u.col : 0) + 8 * h;
       if constexpr (TBF) {
         e.v[s] = *reinterpret_cast<const uint4*>(
             reinterpret_cast<const uint16_t*>(a.E) + id * k + col);
@@ -178,6 +190,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         e.v[2 * s] = p[0];
         e.v[2 * s + 1] = p[1];
       }
+      adv(u);
     }
   };
 
@@ -191,7 +204,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 
   __syncthreads();   // ids, step tables visible
   EChunk e0;
-  eload(e0, 0);
+  Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
+  eload(e0, cg);
   dma(0, 0);
   __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
@@ -249,7 +263,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     // then the next chunk's weight DMA and gathers, in one burst
     // (measured: placing them one per MFMA gap instead ran 6-7 % slower)
     if (c + 1 < nchunks) dma(c + 1, b ^ 1);
-    if (c + 1 < nc0) eload(e, c + 1);
+    if (c + 1 < nc0) eload(e, cg);
     auto bop = [&](int j) {
       if constexpr (TBF) {
         const uint32_t x4[4] = {bxs[j].x, bxs[j].y, bxs[j].z, bxs[j].w};
@@ -263,8 +277,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     };
     // FM second-order part over the same values (DFM.py:114-122)
     auto side = [&](int j) {
-      const int S = 4 * c + j;
-      const int f = S < nS ? S % F : -1;
+      const int f = cs.S < nS ? cs.f : -1;
       if (f == 0) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) { fs[q] = 0.f; fq[q] = 0.f; }
@@ -276,7 +289,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
       }
       if (f == F - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
         const float4* wc =
-            reinterpret_cast<const float4*>(wpl + kFusedMaxF + 16 * (S / F) + 8 * h);
+            reinterpret_cast<const float4*>(wpl + kFusedMaxF + cs.col + 8 * h);
         const float4 w0 = wc[0], w1 = wc[1];
         const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         float d = 0.f;
@@ -284,6 +297,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         for (int q = 0; q < 8; ++q) d += 0.5f * (fs[q] * fs[q] - fq[q]) * wq[q];
         y2 += d;
       }
+      adv(cs);
     };
     run_chunk(b, bop, side);
     __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
