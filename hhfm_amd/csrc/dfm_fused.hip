@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   float y2 = 0.f;
 
   __syncthreads();   // ids, step tables visible
-  EChunk e0;
+  EChunk e0, e1;
   Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
   eload(e0, cg);
   dma(0, 0);
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   // weight DMA and gathers into the freed registers: the compiler's wait on
   // the gathered registers (it cannot count loads across the loop's back
   // edge, so it is a vmcnt(0)) then lands before the new loads, not after.
-  auto chunk0 = [&](int c, EChunk& e) {
+  auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
     const int b = c & 1;
     float v[4][8];
     uint4 bxs[4];
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     // then the next chunk's weight DMA and gathers, in one burst
     // (measured: placing them one per MFMA gap instead ran 6-7 % slower)
     if (c + 1 < nchunks) dma(c + 1, b ^ 1);
-    if (c + 1 < nc0) eload(e, cg);
+    if (c + 1 < nc0) eload(en, cg);
     auto bop = [&](int j) {
       if constexpr (TBF) {
         const uint32_t x4[4] = {bxs[j].x, bxs[j].y, bxs[j].z, bxs[j].w};
@@ -302,7 +302,12 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     run_chunk(b, bop, side);
     __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
   };
-  for (int c = 0; c < nc0; ++c) chunk0(c, e0);
+  // (two register sets alternate, so no copy of the gathered chunk is needed
+  // on the loop's back edge)
+  for (int c = 0; c < nc0; c += 2) {
+    chunk0(c, e0, e1);
+    if (c + 1 < nc0) chunk0(c + 1, e1, e0);
+  }
 
   // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
   uint32_t X[TM][8];
