@@ -3,6 +3,7 @@
 Scoring runs on the gfx950 kernels of afm.hip (exact-fp32 MFMA):
   * ``score_rows`` / ``sess.run(model.out)`` -> hhfm_afm_forward (AFM.py:103-142)
   * ``topk(A, tp)`` -> hhfm_afm_catalog_topk (AFM.py:209-246)
+  * ``partial_fit(data)`` -> hhfm_afm_train_step (AFM.py:144-156, 205-207)
 """
 from __future__ import annotations
 
@@ -114,7 +115,9 @@ class AFM(ScoringModel):
         return super()._run_fetch(fetch, feed)
 
     def partial_fit(self, data):
-        raise NotImplementedError("AFM training (partial_fit) is not implemented yet")
+        """AFM.py:205-207 -> hhfm_afm_train_step (loss, then the update)."""
+        from .training import afm_partial_fit
+        return afm_partial_fit(self, data)
 
 
 class Train(harness.Train):
@@ -137,7 +140,7 @@ class Train(harness.Train):
 
     def train(self):
         from .training import run_training
-        return run_training(self, negatives=2, neg_label=-1)
+        return run_training(self, negatives=2, neg_label=-1, plateau=-0.01, epoch_cap=None)
 
 
 def AFM_main(dataname, factor, Topk, argv=None):

@@ -164,7 +164,7 @@ class Train(harness.Train):
 
     def train(self):
         from .training import run_training
-        return run_training(self, negatives=2, neg_label=-1)
+        return run_training(self, negatives=2, neg_label=-1, epoch_cap=None)
 
 
 def DFM_main(dataname, factor, Topk, argv=None):

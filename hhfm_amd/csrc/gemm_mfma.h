@@ -43,6 +43,9 @@ struct GemmArgs {
   int G;                // grouped dot: group size (16, 32 or 64)
   int mod;              // grouped dot: bias / v are indexed by n % mod
   int64_t ldp;          // grouped dot: row stride of partial
+  int ksplit;           // split-K (epilogue 0): blockIdx.z covers K range
+                        // [z*ksplit, (z+1)*ksplit), ksplit % 32 == 0, and
+  int64_t cz_stride;    // stores to C + z*cz_stride (elements); 0 = no split
 };
 
 // (i, j) of pair p among i<j<F in the reference's loop order (AFM.py:107-110)
@@ -148,7 +151,9 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
   const int wm = wv >> 1, wn = wv & 1;
   const int64_t m0 = (int64_t)blockIdx.x * GBM;
   const int n0 = blockIdx.y * GBN;
-  const int nk = (g.K + BK - 1) / BK;
+  const int kb = g.ksplit ? (int)blockIdx.z * g.ksplit : 0;
+  const int ke = g.ksplit ? min(g.K, kb + g.ksplit) : g.K;
+  const int nk = (ke - kb + BK - 1) / BK;
 
   // each thread stages 2 A chunks and 2 B chunks per K-step
   u32x4_t ra[2], rb[2];
@@ -156,8 +161,8 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int c = tid + 256 * i, r = c / CPR, p = c % CPR;
-      ra[i] = load_a_chunk<BF>(g, m0 + r, kt * BK + p * EL);
-      rb[i] = load_b_chunk<BF>(g, n0 + r, kt * BK + p * EL);
+      ra[i] = load_a_chunk<BF>(g, m0 + r, kb + kt * BK + p * EL);
+      rb[i] = load_b_chunk<BF>(g, n0 + r, kb + kt * BK + p * EL);
     }
   };
   auto sstore = [&](int buf) {
@@ -223,6 +228,7 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
   // ---- epilogue: C/D layout col = l&15, row = 4*(l>>4) + r ----
   const int col_l = l & 15, rq = (l >> 4) * 4;
   if constexpr (EPI == 0) {
+    const int64_t cz = (int64_t)blockIdx.z * g.cz_stride;
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int n = n0 + wn * 64 + 16 * b + col_l;
@@ -238,9 +244,9 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
             if (g.relu) v = fmaxf(v, 0.f);
             if (n >= g.N) v = 0.f;  // zero pad columns: next layer's K padding
             if (g.c_bf16)
-              reinterpret_cast<uint16_t*>(g.C)[m * g.ldc + n] = f2bf(v);
+              reinterpret_cast<uint16_t*>(g.C)[cz + m * g.ldc + n] = f2bf(v);
             else
-              reinterpret_cast<float*>(g.C)[m * g.ldc + n] = v;
+              reinterpret_cast<float*>(g.C)[cz + m * g.ldc + n] = v;
           }
         }
     }
@@ -320,7 +326,8 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
 }
 
 static inline void launch_gemm(const GemmArgs& g, bool bf, int epi, hipStream_t st) {
-  dim3 grid((unsigned)((g.M + GBM - 1) / GBM), (unsigned)((g.N + GBN - 1) / GBN));
+  dim3 grid((unsigned)((g.M + GBM - 1) / GBM), (unsigned)((g.N + GBN - 1) / GBN),
+            g.ksplit ? (unsigned)((g.K + g.ksplit - 1) / g.ksplit) : 1u);
   if (epi == 2) {  // grouped dot (AFM attention logits), f32 only
     hipLaunchKernelGGL((gemm_mfma<false, 2>), grid, dim3(256), 0, st, g);
     return;

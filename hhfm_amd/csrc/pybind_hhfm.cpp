@@ -305,6 +305,32 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_dfm_train_step");
         });
 
+  m.def("afm_train_workspace", [](int64_t B, int F, int k, int A, int64_t M) {
+    size_t ws = 0;
+    check(hhfm_afm_train_workspace(B, F, k, A, M, &ws), "hhfm_afm_train_workspace");
+    return ws;
+  });
+
+  m.def("afm_train_step",
+        [](uptr idx, uptr y, int64_t B, int F, uptr E, uptr w, uptr w0, int64_t M, int k, int A,
+           uptr W, uptr b, uptr pvec, uptr Pv, float lr, float lam, int opt,
+           std::vector<uptr> acc, uptr ws, size_t ws_bytes, uptr loss, uptr stream) {
+          if (opt == 0 && acc.size() != 7)
+            throw py::value_error("acc needs 7 accumulators (E, w, w0, W, b, pvec, P)");
+          std::vector<float*> av(acc.size());
+          for (size_t i = 0; i < acc.size(); ++i) av[i] = P<float>(acc[i]);
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_afm_train_step(P<const int32_t>(idx), P<const float>(y), B, F, P<float>(E),
+                                     P<float>(w), P<float>(w0), M, k, A, P<float>(W), P<float>(b),
+                                     P<float>(pvec), P<float>(Pv), lr, lam, opt,
+                                     av.empty() ? nullptr : av.data(), P<void>(ws), ws_bytes,
+                                     P<float>(loss), P<void>(stream));
+          }
+          check(rc, "hhfm_afm_train_step");
+        });
+
   m.def("topk_dense",
         [](uptr scores, int64_t B, int N, int64_t ld, int K, int base, uptr top_score,
            uptr top_idx, uptr stream) {

@@ -1,4 +1,4 @@
-// H6 — training step (`partial_fit`) for FM and HHFM on gfx950.
+// H6 — training step (`partial_fit`) for FM, HHFM, DeepFM and AFM on gfx950.
 //
 //   hhfm_fm_train_step    replaces sess.run((loss, optimizer)) of FM
 //                         (Newcode/FM.py:123-136, 168-171)
@@ -6,6 +6,8 @@
 //                         (Newcode/OurModel7.py:172-193, 219-228)
 //   hhfm_dfm_train_step   replaces the same for DeepFM
 //                         (Newcode/DFM.py:139-155, 214-217)
+//   hhfm_afm_train_step   replaces the same for AFM
+//                         (Newcode/AFM.py:144-156, 205-207)
 //
 // One wave per batch row computes the forward score(s) and scatters the
 // gradient of the row's loss into dense fp32 gradient buffers with float
@@ -430,6 +432,269 @@ static bool dfm_train_plan(int64_t B, int F, int k, int64_t M, int L, const int3
   return true;
 }
 
+
+// ---------------------------------------------------------------------------
+// AFM training (fp32, AFM.py:103-156): the two pair-shaped products run as
+// exact-fp32 MFMA GEMMs (gemm_mfma.h) over the B·np (row, pair) "combos":
+//   R   = relu(pairs · W + b)           pair-mode A operand (e_i ⊙ e_j formed
+//                                        in the loader), [B·np][A]
+//   DP  = dZ · Wᵀ                       ∂L/∂pairs through the attention MLP
+//   dW  = pairsᵀ · dZ                   split-K over the B·np combos, then a
+//                                        fixed-order sum of the splits
+// and two wave-per-row kernels do the rest: `afm_train_head` (logits,
+// softmax over the row's pairs, out, d = out − y, the softmax backward
+// dlogit = a ⊙ (da − Σ a·da), dZ = dlogit·p ⊙ relu', db, dp, dP, dw; writes
+// dZ and the pair products transposed for the dW GEMM) and `afm_train_scatter`
+// (∂L/∂e_i += dpair ⊙ e_j, ∂L/∂e_j += dpair ⊙ e_i, float atomics into dE).
+// ---------------------------------------------------------------------------
+constexpr int kAfmTrainMaxF = 16;                          // np <= 120
+constexpr int kAfmTrainMaxNp = kAfmTrainMaxF * (kAfmTrainMaxF - 1) / 2;
+constexpr int kAfmTrainMaxKA = 256;                        // k, A <= 256
+constexpr int kAfmSplitK = 512;                            // combos per dW split
+
+__global__ __launch_bounds__(256) void afm_train_head(
+    const int32_t* __restrict__ idx, const float* __restrict__ y, int64_t B, int F,
+    const float* __restrict__ E, const float* __restrict__ w, const float* __restrict__ w0,
+    int64_t M, int k, int A, const float* __restrict__ R, const float* __restrict__ pvec,
+    const float* __restrict__ P, float* __restrict__ Gz, float* __restrict__ PT,
+    float* __restrict__ GzT, int64_t Kp, float* __restrict__ att, float* __restrict__ gvec,
+    float* __restrict__ dP, float* __restrict__ dpv, float* __restrict__ db,
+    float* __restrict__ dw, float* __restrict__ scal) {
+  constexpr int NC = kAfmTrainMaxKA / kWave;
+  __shared__ float sp_all[4][kAfmTrainMaxNp], lg_all[4][kAfmTrainMaxNp];
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float* sp = sp_all[wv];
+  float* lg = lg_all[wv];
+  const int np = F * (F - 1) / 2;
+  float accP[NC], accV[NC], accB[NC];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) accP[j] = accV[j] = accB[j] = 0.f;
+  float sg = 0.f, sl = 0.f;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* x = idx + m * F;
+    const int64_t c0 = m * np;   // first combo of this row
+    // s_p = P·(e_i ⊙ e_j)   (lanes over k; one wave sum per pair and chunk)
+    for (int p = l; p < np; p += kWave) sp[p] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < NC; ++kc) {
+      const int c = l + kWave * kc;
+      if (kc * kWave >= k) break;
+      float ev[kAfmTrainMaxF];
+#pragma unroll
+      for (int f = 0; f < kAfmTrainMaxF; ++f)
+        ev[f] = (f < F && c < k) ? E[(int64_t)clamp_id(x[f], M) * k + c] : 0.f;
+      const float pc = c < k ? P[c] : 0.f;
+      int p = 0;
+#pragma unroll
+      for (int i = 0; i < kAfmTrainMaxF; ++i)
+#pragma unroll
+        for (int j = i + 1; j < kAfmTrainMaxF; ++j)
+          if (j < F) {
+            const float s = group_sum<kWave>(ev[i] * ev[j] * pc);
+            if (l == 0) sp[p] += s;
+            ++p;
+          }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // logit_p = Σ_a pvec_a · R[p][a]   (lanes over A)
+    for (int p = 0; p < np; ++p) {
+      float t = 0.f;
+      for (int a = l; a < A; a += kWave) t = fmaf(pvec[a], R[(c0 + p) * A + a], t);
+      t = group_sum<kWave>(t);
+      if (l == 0) lg[p] = t;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // softmax over the row's pairs (AFM.py:125, max subtracted), out, d
+    float mx = -__builtin_huge_valf();
+    for (int p = l; p < np; p += kWave) mx = fmaxf(mx, lg[p]);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, kWave));
+    float se = 0.f;
+    for (int p = l; p < np; p += kWave) se += expf(lg[p] - mx);
+    se = group_sum<kWave>(se);
+    float os = 0.f;
+    for (int p = l; p < np; p += kWave) os += expf(lg[p] - mx) / se * sp[p];
+    os = group_sum<kWave>(os);
+    float fb = 0.f;
+    for (int f = l; f < F; f += kWave) fb += w[clamp_id(x[f], M)];
+    fb = group_sum<kWave>(fb);
+    const float out = (os + fb) + w0[0];
+    const float g = out - y[m];                      // d l2_loss(y − out) / d out
+    sg += g;
+    sl += 0.5f * g * g;
+    // da_p = g·s_p, dlogit_p = a_p (da_p − Σ a·da)
+    float t = 0.f;
+    for (int p = l; p < np; p += kWave) t += expf(lg[p] - mx) / se * (g * sp[p]);
+    t = group_sum<kWave>(t);
+    for (int p = l; p < np; p += kWave) {
+      const float a = expf(lg[p] - mx) / se;
+      att[c0 + p] = a;
+      lg[p] = a * (g * sp[p] - t);                   // lg now holds dlogit
+      sp[p] = a;                                     // sp now holds att
+    }
+    if (l == 0) gvec[m] = g;
+    __builtin_amdgcn_wave_barrier();
+    // dZ = dlogit·p ⊙ relu'(z)  (lanes over A), written row-major and transposed
+#pragma unroll
+    for (int ac = 0; ac < NC; ++ac) {
+      const int a = l + kWave * ac;
+      if (ac * kWave >= A) break;
+      if (a < A) {
+        const float pa = pvec[a];
+        for (int p = 0; p < np; ++p) {
+          const float r = R[(c0 + p) * A + a];
+          const float dl = lg[p];
+          accV[ac] = fmaf(dl, r, accV[ac]);
+          const float dz = r > 0.f ? dl * pa : 0.f;
+          accB[ac] += dz;
+          Gz[(c0 + p) * A + a] = dz;
+          GzT[a * Kp + c0 + p] = dz;
+        }
+      }
+    }
+    // afm = Σ a_p (e_i ⊙ e_j) -> dP; pair products transposed for the dW GEMM
+#pragma unroll
+    for (int kc = 0; kc < NC; ++kc) {
+      const int c = l + kWave * kc;
+      if (kc * kWave >= k) break;
+      if (c < k) {
+        float ev[kAfmTrainMaxF];
+#pragma unroll
+        for (int f = 0; f < kAfmTrainMaxF; ++f)
+          ev[f] = f < F ? E[(int64_t)clamp_id(x[f], M) * k + c] : 0.f;
+        float afm = 0.f;
+        int p = 0;
+#pragma unroll
+        for (int i = 0; i < kAfmTrainMaxF; ++i)
+#pragma unroll
+          for (int j = i + 1; j < kAfmTrainMaxF; ++j)
+            if (j < F) {
+              const float pr = ev[i] * ev[j];
+              afm = fmaf(sp[p], pr, afm);
+              PT[c * Kp + c0 + p] = pr;
+              ++p;
+            }
+        accP[kc] = fmaf(g, afm, accP[kc]);
+      }
+    }
+    for (int f = l; f < F; f += kWave) atomicAdd(&dw[clamp_id(x[f], M)], g);
+    __builtin_amdgcn_wave_barrier();   // sp / lg are rewritten by the next row
+  }
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = l + kWave * j;
+    if (c < k && accP[j] != 0.f) atomicAdd(&dP[c], accP[j]);
+    if (c < A && accV[j] != 0.f) atomicAdd(&dpv[c], accV[j]);
+    if (c < A && accB[j] != 0.f) atomicAdd(&db[c], accB[j]);
+  }
+  if (l == 0) {   // g is wave-uniform
+    atomicAdd(&scal[0], sg);
+    atomicAdd(&scal[1], sl);
+  }
+}
+
+// dE[x_f][c] += Σ_{pairs ∋ f} (DP + a_p·d·P_c) ⊙ e_other   (wave per row, lanes over k)
+__global__ __launch_bounds__(256) void afm_train_scatter(
+    const int32_t* __restrict__ idx, int64_t B, int F, const float* __restrict__ E, int64_t M,
+    int k, const float* __restrict__ DP, const float* __restrict__ att,
+    const float* __restrict__ gvec, const float* __restrict__ P, float* __restrict__ dE) {
+  const int l = threadIdx.x & 63;
+  const int np = F * (F - 1) / 2;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  for (int64_t m = wave; m < B; m += nwave) {
+    const int32_t* x = idx + m * F;
+    const int64_t c0 = m * np;
+    const float g = gvec[m];
+    for (int c = l; c < k; c += kWave) {
+      float ev[kAfmTrainMaxF], de[kAfmTrainMaxF];
+#pragma unroll
+      for (int f = 0; f < kAfmTrainMaxF; ++f) {
+        ev[f] = f < F ? E[(int64_t)clamp_id(x[f], M) * k + c] : 0.f;
+        de[f] = 0.f;
+      }
+      const float gp = g * P[c];
+      int p = 0;
+#pragma unroll
+      for (int i = 0; i < kAfmTrainMaxF; ++i)
+#pragma unroll
+        for (int j = i + 1; j < kAfmTrainMaxF; ++j)
+          if (j < F) {
+            const float d = fmaf(att[c0 + p], gp, DP[(c0 + p) * k + c]);
+            de[i] = fmaf(d, ev[j], de[i]);
+            de[j] = fmaf(d, ev[i], de[j]);
+            ++p;
+          }
+#pragma unroll
+      for (int f = 0; f < kAfmTrainMaxF; ++f)
+        if (f < F) atomicAdd(&dE[(int64_t)clamp_id(x[f], M) * k + c], de[f]);
+    }
+  }
+}
+
+// zero the K padding [n, Kp) of `rows` transposed rows of stride Kp
+__global__ __launch_bounds__(256) void zero_cols(float* __restrict__ T, int rows, int64_t Kp,
+                                                 int64_t n) {
+  const int pad = (int)(Kp - n);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (int64_t)rows * pad;
+       i += (int64_t)gridDim.x * blockDim.x)
+    T[(i / pad) * Kp + n + i % pad] = 0.f;
+}
+
+// dW[i] = Σ_s part[s][i] in split order (deterministic)
+__global__ __launch_bounds__(256) void sum_splits(const float* __restrict__ part, int S,
+                                                  int64_t n, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int z = 0; z < S; ++z) s += part[z * n + i];
+    out[i] = s;
+  }
+}
+
+struct AfmTrainPlan {
+  int np;
+  int64_t n, Kp;
+  int S;
+  int64_t off_Wt, off_R, off_Gz, off_T, off_DP, off_att, off_g, off_part;
+  int64_t off_dE, off_dw, off_dW, off_db, off_dpv, off_dP, off_scal;
+  int64_t total;   // floats
+};
+
+static bool afm_train_plan(int64_t B, int F, int k, int A, int64_t M, AfmTrainPlan& p) {
+  if (F < 2 || F > kAfmTrainMaxF || k < 4 || k % 4 || k > kAfmTrainMaxKA || A < 4 || A % 4 ||
+      A > kAfmTrainMaxKA || B < 0 || M < 1)
+    return false;
+  p = AfmTrainPlan{};
+  p.np = F * (F - 1) / 2;
+  p.n = B * p.np;
+  if (p.n > (int64_t)1 << 30) return false;
+  p.Kp = pad8(p.n > 0 ? p.n : 1);
+  p.S = (int)((p.Kp + kAfmSplitK - 1) / kAfmSplitK);
+  int64_t o = 0;
+  auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  p.off_Wt = take((int64_t)A * k);
+  p.off_R = take(p.n * A);
+  p.off_Gz = take(p.n * A);
+  p.off_T = take((int64_t)(k + A) * p.Kp);   // PT [k][Kp] then GzT [A][Kp]
+  p.off_DP = take(p.n * k);
+  p.off_att = take(p.n);
+  p.off_g = take(B);
+  p.off_part = take((int64_t)p.S * k * A);
+  // zero-initialised, kept zeroed by the step
+  p.off_dE = take(M * k);
+  p.off_dw = take(M);
+  p.off_dW = take((int64_t)k * A);
+  p.off_db = take(A);
+  p.off_dpv = take(A);
+  p.off_dP = take(k);
+  p.off_scal = take(16);
+  p.total = o;
+  return true;
+}
+
 }  // namespace hhfm
 
 using namespace hhfm;
@@ -648,5 +913,125 @@ extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B
   hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, bp, acc_of(3 + 2 * L), scal, lr,
                      optimizer);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lambda_l2, loss);
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_afm_train_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
+                                        int64_t features_M, size_t* ws_bytes) {
+  AfmTrainPlan p;
+  if (!ws_bytes || !afm_train_plan(B, F, k, A, features_M, p)) return HHFM_EINVAL;
+  *ws_bytes = (size_t)p.total * 4;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F,
+                                   float* E, float* w, float* w0, int64_t features_M, int32_t k,
+                                   int32_t A, float* W, float* b, float* pvec, float* P,
+                                   float lr, float lambda_att, int32_t optimizer,
+                                   float* const* acc, void* workspace, size_t ws_bytes,
+                                   float* loss, void* stream) {
+  AfmTrainPlan p;
+  if (!afm_train_plan(B, F, k, A, features_M, p)) return HHFM_EINVAL;
+  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!idx || !y || !E || !w || !w0 || !W || !b || !pvec || !P || !loss || !workspace)
+    return HHFM_EINVAL;
+  if (optimizer == OPT_ADAGRAD) {   // acc: E, w, w0, W, b, pvec, P
+    if (!acc) return HHFM_EINVAL;
+    for (int i = 0; i < 7; ++i)
+      if (!acc[i]) return HHFM_EINVAL;
+  }
+  if (ws_bytes < (size_t)p.total * 4) return HHFM_EWORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  auto at = [&](int64_t off) { return ws + off; };
+  float* scal = at(p.off_scal);
+  float* PT = at(p.off_T);
+  float* GzT = PT + (int64_t)k * p.Kp;
+  auto acc_of = [&](int i) { return optimizer == OPT_ADAGRAD ? acc[i] : (float*)nullptr; };
+
+  if (B > 0) {
+    // Wᵀ [A][k] for the forward GEMM
+    hipLaunchKernelGGL(tr_pad, dim3((unsigned)((k + 31) / 32), (unsigned)((A + 31) / 32)),
+                       dim3(256), 0, st, W, (int64_t)k, A, (int64_t)A, (const float*)nullptr,
+                       (int64_t)0, at(p.off_Wt), (int64_t)k, (int64_t)k);
+    {   // R = relu(pairs · W + b)   (AFM.py:117-121)
+      GemmArgs g{};
+      g.M = p.n;
+      g.N = A;
+      g.K = k;
+      g.pair_mode = 1;
+      g.P = p.np;
+      g.gidx = idx;
+      g.T = E;
+      g.Mtab = features_M;
+      g.F = F;
+      g.kf = k;
+      g.Bt = at(p.off_Wt);
+      g.ldb = k;
+      g.bias = b;
+      g.relu = 1;
+      g.C = at(p.off_R);
+      g.ldc = A;
+      launch_gemm(g, false, 0, st);
+    }
+    // a few rows per wave: the per-wave dP / dp / db flush is k + 2A same-address atomics
+    const unsigned hb = (unsigned)std::min<int64_t>(256, (B + 3) / 4);
+    hipLaunchKernelGGL(afm_train_head, dim3(hb), dim3(256), 0, st, idx, y,
+                       B, F, E, w, w0, features_M, k, A, at(p.off_R), pvec, P, at(p.off_Gz), PT,
+                       GzT, p.Kp, at(p.off_att), at(p.off_g), at(p.off_dP), at(p.off_dpv),
+                       at(p.off_db), at(p.off_dw), scal);
+    if (p.Kp > p.n)
+      hipLaunchKernelGGL(zero_cols, dim3(grid_for_n((int64_t)(k + A) * (p.Kp - p.n))),
+                         dim3(256), 0, st, PT, k + A, p.Kp, p.n);
+    {   // DP = dZ · Wᵀ   (Bt = W [k][A])
+      GemmArgs g{};
+      g.M = p.n;
+      g.N = k;
+      g.K = A;
+      g.A = at(p.off_Gz);
+      g.lda = A;
+      g.Bt = W;
+      g.ldb = A;
+      g.C = at(p.off_DP);
+      g.ldc = k;
+      launch_gemm(g, false, 0, st);
+    }
+    {   // dW = pairsᵀ · dZ, split over the combos
+      GemmArgs g{};
+      g.M = k;
+      g.N = A;
+      g.K = (int)p.Kp;
+      g.A = PT;
+      g.lda = p.Kp;
+      g.Bt = GzT;
+      g.ldb = p.Kp;
+      g.C = at(p.off_part);
+      g.ldc = A;
+      g.ksplit = kAfmSplitK;
+      g.cz_stride = (int64_t)k * A;
+      launch_gemm(g, false, 0, st);
+      hipLaunchKernelGGL(sum_splits, dim3(grid_for_n((int64_t)k * A)), dim3(256), 0, st,
+                         (const float*)at(p.off_part), p.S, (int64_t)k * A, at(p.off_dW));
+    }
+    hipLaunchKernelGGL(afm_train_scatter, dim3(grid_for_n(B * 64)), dim3(256), 0, st, idx, B, F,
+                       E, features_M, k, at(p.off_DP), at(p.off_att), at(p.off_g), P,
+                       at(p.off_dE));
+  }
+  const int64_t nE = features_M * k;
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, at(p.off_dE),
+                     acc_of(0), nE, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(features_M)), dim3(256), 0, st, w,
+                     at(p.off_dw), acc_of(1), features_M, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, w0, acc_of(2), scal, lr, optimizer);
+  // l2_regularizer(λ)(attention_W) only (AFM.py:146)
+  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n((int64_t)k * A)), dim3(256), 0, st, W,
+                     at(p.off_dW), acc_of(3), (int64_t)k * A, lr, lambda_att, optimizer, scal + 2);
+  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, b, at(p.off_db), acc_of(4),
+                     (int64_t)A, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, pvec, at(p.off_dpv), acc_of(5),
+                     (int64_t)A, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, P, at(p.off_dP), acc_of(6),
+                     (int64_t)k, lr, 0.f, optimizer, (float*)nullptr);
+  hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lambda_att, loss);
   return (int)hipGetLastError();
 }

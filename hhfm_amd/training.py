@@ -1,5 +1,5 @@
-"""Training surface (§8f "next" H6): ``partial_fit`` on the gfx950 train-step
-kernels and the reference's epoch loops.
+"""Training surface (§8f "next" H6): ``partial_fit`` of FM, HHFM, DeepFM and
+AFM on the gfx950 train-step kernels and the reference's epoch loops.
 
 * FM / AFM / DFM loop — FM.py:221-282: each epoch NG=2 negatives per
   positive (label 0 for FM, -1 for AFM/DFM, FM.py:248 / AFM.py:317), shuffle,
@@ -131,6 +131,45 @@ def dfm_partial_fit(model, data) -> float:
     return float(st["loss"].item())
 
 
+def afm_partial_fit(model, data) -> float:
+    """AFM.partial_fit (AFM.py:205-207): one TF step on every variable, loss
+    l2_loss(y − out) + l2_regularizer(λ)(attention_W) when λ > 0 (AFM.py:144-148)."""
+    opt = _opt_code(model)
+    if any(float(x) != 1.0 for x in np.ravel(model.keep)):
+        raise NotImplementedError("dropout keep < 1 is not implemented")
+    W = model.weights
+    names = ["feature_embeddings", "feature_bias", "bias", "attention_W", "attention_b",
+             "attention_p", "prediction"]
+    st = getattr(model, "_train_state", None)
+    if st is None:
+        if model.table_dtype != torch.float32:
+            raise NotImplementedError("training runs on fp32 tables")
+        st = {n: torch.full_like(W[n], 0.1) for n in names}
+        st["loss"] = torch.zeros(1, dtype=torch.float32, device=model.device)
+        st["ws"], st["ws_rows"] = None, 0
+        model._train_state = st
+    X = model._idx(data["X"])
+    y = torch.as_tensor(np.asarray(data["Y"], np.float32).reshape(-1)).to(model.device)
+    B, F = X.shape
+    M, k = W["feature_embeddings"].shape
+    A = W["attention_W"].shape[1]
+    nat = native()
+    if st["ws"] is None or st["ws_rows"] < B:
+        nbytes = nat.afm_train_workspace(B, F, k, A, M)
+        st["ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=model.device)
+        st["ws_rows"] = B
+    lam = float(model.lamda_attention) if model.lamda_attention > 0 else 0.0
+    ptr = lambda n: W[n].data_ptr()  # noqa: E731
+    nat.afm_train_step(X.data_ptr(), y.data_ptr(), B, F, ptr("feature_embeddings"),
+                       ptr("feature_bias"), ptr("bias"), M, k, A, ptr("attention_W"),
+                       ptr("attention_b"), ptr("attention_p"), ptr("prediction"),
+                       float(model.learning_rate), lam, opt,
+                       [st[n].data_ptr() for n in names] if opt == 0 else [],
+                       st["ws"].data_ptr(), st["ws"].numel(), st["loss"].data_ptr(),
+                       ops._stream(model.device))
+    return float(st["loss"].item())
+
+
 def _log(tr, line):
     print(line)
     path = getattr(tr.args, "result_file", None)
@@ -150,8 +189,11 @@ def _report(tr, head, t_epoch, t_eval0, res):
          % (head, t_epoch, a1, a2, tk[0], tk[1], tk[2], time() - t_eval0))
 
 
-def run_training(tr, negatives=2, neg_label=0):
-    """FM.py:221-282 (also AFM.py:290-351, DFM.py:259-320)."""
+def run_training(tr, negatives=2, neg_label=0, plateau=-0.0075, epoch_cap=100):
+    """FM.py:221-282 (also AFM.py:290-351, DFM.py:259-320).  The loss-plateau
+    stop (Result == 1) is ``plateau`` = −0.0075 with a 100-epoch cap in FM
+    (FM.py:261-262), −0.0075 without a cap in DFM (DFM.py:299-300) and −0.01
+    without a cap in AFM (AFM.py:330-331)."""
     args = tr.args
     t2 = time()
     if args.Result == 0:
@@ -180,8 +222,8 @@ def run_training(tr, negatives=2, neg_label=0):
         if args.Result == 1 and epoch > 30:
             n = 3
             le = np.array(tr.loss_epoch)
-            cond = np.sum((le[-1 - n:-1] / le[-2 - n:-2] - 1) > -0.0075)
-            if cond == n or epoch > 100:
+            cond = np.sum((le[-1 - n:-1] / le[-2 - n:-2] - 1) > plateau)
+            if cond == n or (epoch_cap is not None and epoch > epoch_cap):
                 _report(tr, "%s%s Epoch %d" % (args.dataset, tr.method, epoch), t2 - t1, t2,
                         _evaluate(tr))
                 break

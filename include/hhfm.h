@@ -241,6 +241,25 @@ int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F
                         float* const* acc, void* workspace, size_t ws_bytes, float* loss,
                         void* stream);
 
+/* AFM (AFM.py:103-156, 205-207; attention = 1, keep = [1, 1]):
+ *   loss = Σ (y − out)²/2 + λ·‖attention_W‖²/2
+ * one step of TF Adagrad (optimizer 0) or gradient descent (1) on every
+ * variable, in place: E [M][k], w [M], w0 (device float), W = attention_W
+ * [k][A] row-major, b = attention_b [A], pvec = attention_p [A], P =
+ * prediction [k].  acc (Adagrad): 7 device accumulators in the order E, w,
+ * w0, W, b, pvec, P, initialised to 0.1 by the caller.  The workspace
+ * (hhfm_afm_train_workspace bytes for batches of at most B rows) must be
+ * zero-filled once; the step keeps its gradient regions zeroed.
+ * Requires 2 <= F <= 16, k and A multiples of 4 and <= 256.  Replaces
+ * sess.run((loss, optimizer)) of AFM.partial_fit (AFM.py:205-207). */
+int hhfm_afm_train_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
+                             int64_t features_M, size_t* ws_bytes);
+int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F, float* E,
+                        float* w, float* w0, int64_t features_M, int32_t k, int32_t A,
+                        float* W, float* b, float* pvec, float* P, float lr,
+                        float lambda_att, int32_t optimizer, float* const* acc,
+                        void* workspace, size_t ws_bytes, float* loss, void* stream);
+
 /* tf.nn.top_k(scores, K) over a materialised score matrix [B][ld] (first N
  * columns), K <= 64; ids reported as global_item_base + column. */
 int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,

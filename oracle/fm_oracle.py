@@ -413,3 +413,68 @@ def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="
     Wp = upd(Wp, dWp, "Wp")
     bp = upd(np.float32(bp), dbp, "bp")
     return loss, E, w, layers, biases, Wp, F32(bp), acc
+
+
+def afm_train_step(X, y, E, w, w0, W, b, pvec, P, acc, lr, lam, optimizer="adagrad"):
+    """AFM partial_fit (AFM.py:144-156, 205-207), attention=1, keep=[1,1]:
+    loss = l2_loss(y − out) + l2_regularizer(λ)(attention_W) = Σ(y−out)²/2
+    + λ·ΣW²/2, one TF step on every variable (feature_embeddings,
+    feature_bias, bias, attention_W/b/p, prediction).  Softmax backward
+    dlogit = a ⊙ (da − Σ a·da); relu' where z = pW + b > 0 (TF ReluGrad).
+    acc: dict of accumulators keyed E, w, w0, W, b, p, P.
+    Returns (loss, E, w, w0, W, b, pvec, P, acc)."""
+    X = np.asarray(X, np.int64)
+    y = np.asarray(y, F32).reshape(-1)
+    E = np.asarray(E, F32)
+    w = np.asarray(w, F32).reshape(-1)
+    W = np.asarray(W, F32)
+    b = np.asarray(b, F32).reshape(-1)
+    pvec = np.asarray(pvec, F32).reshape(-1)
+    P = np.asarray(P, F32).reshape(-1)
+    B, F = X.shape
+    k, A = W.shape
+    e = E[X]                                                          # :104
+    pr = _pairs(e)                                                    # :107-112 [B,np,k]
+    z = (np.matmul(pr.reshape(-1, k), W).astype(F32) + b).reshape(B, -1, A)   # :117
+    r = np.maximum(z, 0)
+    logit = (pvec * r).sum(-1, dtype=F32)                             # :121-124 [B,np]
+    ex = np.exp(logit - logit.max(1, keepdims=True))
+    att = (ex / ex.sum(1, keepdims=True)).astype(F32)                 # :125
+    afm = (att[:, :, None] * pr).sum(1, dtype=F32)                    # :130 [B,k]
+    out = np.matmul(afm, P).astype(F32) + w[X].sum(1, dtype=F32) + F32(w0)   # :138-142
+    res = y - out
+    loss = F32(np.sum(res.astype(np.float64) ** 2) / 2
+               + lam * np.sum(W.astype(np.float64) ** 2) / 2)        # :146-149
+    g = -res                                                          # d loss / d out
+    dP = np.matmul(afm.T, g).astype(F32)
+    dw0 = F32(g.sum(dtype=np.float64))
+    s = np.matmul(pr, P).astype(F32)                                  # [B,np] = pr·P
+    da = g[:, None] * s
+    dlogit = att * (da - (att * da).sum(1, keepdims=True))
+    dpvec = (dlogit[:, :, None] * r).sum((0, 1), dtype=F32)
+    dz = (dlogit[:, :, None] * pvec * (z > 0)).astype(F32)            # [B,np,A]
+    db = dz.sum((0, 1), dtype=F32)
+    dW = np.matmul(pr.reshape(-1, k).T, dz.reshape(-1, A)).astype(F32) + F32(lam) * W
+    dpr = att[:, :, None] * (g[:, None] * P[None, :])[:, None, :] + np.matmul(dz, W.T).astype(F32)
+    de = np.zeros_like(e)
+    p = 0
+    for i in range(F):
+        for j in range(i + 1, F):
+            de[:, i] += dpr[:, p] * e[:, j]
+            de[:, j] += dpr[:, p] * e[:, i]
+            p += 1
+    dE = np.zeros_like(E)
+    dw = np.zeros_like(w)
+    for f in range(F):
+        np.add.at(dE, X[:, f], de[:, f])
+        np.add.at(dw, X[:, f], g)
+    acc = {key: np.asarray(v, F32).copy() for key, v in acc.items()}
+
+    def upd(var, grad, key):
+        if optimizer == "adagrad":
+            var, acc[key] = tf_adagrad(var, grad, acc[key], lr)
+            return var
+        return (var - F32(lr) * grad).astype(F32)
+
+    return (loss, upd(E, dE, "E"), upd(w, dw, "w"), F32(upd(np.float32(w0), dw0, "w0")),
+            upd(W, dW, "W"), upd(b, db, "b"), upd(pvec, dpvec, "p"), upd(P, dP, "P"), acc)

@@ -165,3 +165,56 @@ def test_dfm_train_loop_end_to_end(tmp_path):
     losses = t.train()
     assert len(losses) == 2 and losses[1] < losses[0]
     assert "DFM Epoch 1" in open(tmp_path / "result.txt").read()
+
+
+@pytest.mark.parametrize("k,A,ctx,B,opt", [
+    (64, 64, (7, 2, 3), 1000, "AdagradOptimizer"),       # Frappe F=5, the reference's k=A
+    (16, 32, (5, 4, 6, 3, 7, 2, 2, 3, 4, 3), 301, "AdagradOptimizer"),   # F=12 (resturant/ml width), ragged
+    (8, 4, (), 7, "GradientDescentOptimizer"),            # F=2: one pair, tiny batch
+    (128, 128, (7, 2, 3), 600, "AdagradOptimizer"),       # main.py's factor 128
+])
+def test_afm_partial_fit_matches_oracle(k, A, ctx, B, opt):
+    """AFM partial_fit (AFM.py:144-156, 205-207): every variable after two
+    steps vs the oracle's TF-semantics step."""
+    from hhfm_amd.AFM import AFM
+    rng = np.random.default_rng(k + A + B)
+    nu, ni = 60, 200
+    X, M = _rows(rng, 2 * B, nu, ni, ctx)
+    F = X.shape[1]
+    m = AFM(nu, ni, M, 1, [A, k], None, 0.1, 100.0, [1, 1], opt, 0.999, F)
+    W = m.get_weights()
+    W["feature_bias"] = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    W["prediction"] = rng.normal(1, 0.2, (k, 1)).astype(np.float32)
+    m.set_weights(feature_bias=W["feature_bias"], prediction=W["prediction"])
+    names = ["feature_embeddings", "feature_bias", "bias", "attention_W", "attention_b",
+             "attention_p", "prediction"]
+    keys = ["E", "w", "w0", "W", "b", "p", "P"]
+    cur = [np.asarray(W[n], np.float32) for n in names]
+    acc = {kk: np.full_like(v, 0.1) for kk, v in zip(keys, cur)}
+    o = "adagrad" if opt == "AdagradOptimizer" else "sgd"
+    for step in range(2):
+        Xb = X[step * B:(step + 1) * B]
+        y = rng.choice([1.0, -1.0], B).astype(np.float32)[:, None]
+        loss = m.partial_fit({"X": Xb, "Y": y})
+        rl, *new, acc = orc.afm_train_step(Xb, y, *cur, acc, 0.1, 100.0, optimizer=o)
+        assert np.isclose(loss, rl, rtol=1e-5), (loss, rl)
+        G = m.get_weights()
+        for n, v_new, v_old in zip(names, new, cur):
+            got = np.asarray(G[n], np.float32).reshape(np.shape(v_new))
+            _close_update(got, np.asarray(v_new, np.float32), np.asarray(v_old, np.float32))
+        cur = [np.asarray(v, np.float32).reshape(np.shape(c)) for v, c in zip(new, cur)]
+    # the scoring path sees the updated weights
+    Xs = X[:50]
+    ref = orc.afm_out(Xs, cur[0], cur[1], cur[2], cur[3], cur[4], cur[5], cur[6])[:, 0]
+    got = m.score_rows(Xs)[:, 0]
+    assert np.allclose(got, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+def test_afm_train_loop_end_to_end(tmp_path):
+    from hhfm_amd.AFM import Train
+    np.random.seed(2016)
+    t = Train(_args(tmp_path, hidden_factor="[16,16]", keep="[1,1]", lamda_attention=100.0,
+                    attention=1, decay=0.999, activation="relu"))
+    losses = t.train()
+    assert len(losses) == 2 and losses[1] < losses[0]
+    assert "AFM Epoch 1" in open(tmp_path / "result.txt").read()

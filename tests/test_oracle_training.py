@@ -119,3 +119,50 @@ def test_tf_adagrad_semantics():
     v1, a1 = orc.tf_adagrad(v, g, a, 0.1)
     assert a1[0] == np.float32(0.35)
     assert np.isclose(v1[0], 1.0 - 0.1 * 0.5 / np.sqrt(0.35))
+
+
+def test_afm_gradient_matches_finite_differences():
+    """AFM (AFM.py:144-156): every variable's gradient, incl. a repeated id."""
+    rng = np.random.default_rng(3)
+    M, k, A, B, F, lam = 25, 4, 8, 10, 4, 0.3
+    X = rng.integers(0, M, (B, F))
+    X[0, 2] = X[0, 1]
+    y = rng.choice([1.0, -1.0], B)
+    E, w = rng.normal(0, 0.5, (M, k)), rng.normal(0, 0.3, M)
+    W, b = rng.normal(0, 0.6, (k, A)), rng.normal(0, 0.3, (1, A))
+    pv, P = rng.normal(0, 1, A), rng.normal(1, 0.3, (k, 1))
+    w0 = 0.05
+    pairs = [(i, j) for i in range(F) for j in range(i + 1, F)]
+
+    def loss(E, w, w0, W, b, pv, P):
+        e = E[X]
+        pr = np.stack([e[:, i] * e[:, j] for i, j in pairs], 1)
+        lg = (pv * np.maximum(pr @ W + b, 0)).sum(-1)
+        a = np.exp(lg - lg.max(1, keepdims=True))
+        a /= a.sum(1, keepdims=True)
+        out = (a[:, :, None] * pr).sum(1) @ P[:, 0] + w[X].sum(1) + w0
+        return ((y - out) ** 2).sum() / 2 + lam * (W ** 2).sum() / 2
+
+    lr = 1e-3
+    l0, E1, w1, w01, W1, b1, pv1, P1, _ = orc.afm_train_step(X, y, E, w, w0, W, b, pv, P, {},
+                                                             lr, lam, optimizer="sgd")
+    args = [E, w, np.array([w0]), W, b, pv, P]
+    assert abs(l0 - loss(E, w, w0, W, b, pv, P)) < 1e-4 * abs(l0)
+
+    def fd(which, i, eps=1e-5):
+        def f(a):
+            v = list(args)
+            v[which] = a
+            return loss(v[0], v[1], v[2][0], *v[3:])
+        a = args[which].astype(np.float64).copy()
+        a[i] += eps
+        lp = f(a)
+        a[i] -= 2 * eps
+        return (lp - f(a)) / (2 * eps)
+
+    new = [E1, w1, np.array([w01]), W1, b1.reshape(1, -1), pv1, P1.reshape(-1, 1)]
+    for which, i in [(0, (X[0, 1], 2)), (0, (X[4, 3], 0)), (1, (X[2, 1],)), (2, (0,)),
+                     (3, (1, 5)), (3, (3, 0)), (4, (0, 6)), (5, (2,)), (6, (1, 0))]:
+        grad = (args[which].astype(np.float32)[i] - new[which][i]) / lr
+        ref = fd(which, i)
+        assert np.isclose(grad, ref, rtol=3e-3, atol=3e-4), (which, i, grad, ref)
