@@ -39,18 +39,23 @@ __global__ __launch_bounds__(256) void afm_rows_finish(
   const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
   for (int64_t m = wave; m < B; m += nwave) {
     const int32_t* x = idx + m * F;
-    // logits of this row's pairs (lane p holds pair p; np <= 64 enforced)
-    float lg = kNegInf;
+    // logits of this row's pairs: lane l holds pairs l and l + 64 (np <= 120)
+    float lg0 = kNegInf, lg1 = kNegInf;
     if (l < np) {
-      lg = 0.f;
-      for (int t = 0; t < ntl; ++t) lg += logit_part[((m * np) + l) * ntl + t];
+      lg0 = 0.f;
+      for (int t = 0; t < ntl; ++t) lg0 += logit_part[((m * np) + l) * ntl + t];
     }
-    float mx = lg;
+    if (l + kWave < np) {
+      lg1 = 0.f;
+      for (int t = 0; t < ntl; ++t) lg1 += logit_part[((m * np) + l + kWave) * ntl + t];
+    }
+    float mx = fmaxf(lg0, lg1);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, kWave));
-    const float e = l < np ? expf(lg - mx) : 0.f;
-    const float s = group_sum<kWave>(e);
-    const float att = e / s;                      // tf.nn.softmax(axis=1), AFM.py:125
+    const float e0 = l < np ? expf(lg0 - mx) : 0.f;
+    const float e1 = l + kWave < np ? expf(lg1 - mx) : 0.f;
+    const float s = group_sum<kWave>(e0 + e1);
+    const float att0 = e0 / s, att1 = e1 / s;     // tf.nn.softmax(axis=1), AFM.py:125
     float bil = 0.f;
     // uniform loop: every lane takes part in the shuffles (att of pair p
     // lives in lane p, which may lie beyond k)
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(256) void afm_rows_finish(
       for (int p = 0; p < np; ++p) {
         int i, j;
         pair_ij(p, F, i, j);
-        const float ap = __shfl(att, p, kWave);
+        const float ap = p < kWave ? __shfl(att0, p, kWave) : __shfl(att1, p - kWave, kWave);
         if (in)
           afm += ap * (tab(E, t_bf16, clamp_id(x[i], M), k, c) *
                        tab(E, t_bf16, clamp_id(x[j], M), k, c));
@@ -570,7 +575,7 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
                                 float w0, const float* Wt, const float* att_b,
                                 const float* att_p, int32_t A, const float* P, float* out,
                                 void* workspace, size_t ws_bytes, void* stream) {
-  if (B < 0 || F < 2 || F > 11 || k < 1 || A < 1 || features_M < 1) return HHFM_EINVAL;
+  if (B < 0 || F < 2 || F > 16 || k < 1 || A < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (k % 4) return HHFM_EUNSUPPORTED;
   if (B == 0) return HHFM_OK;

@@ -173,7 +173,7 @@ int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t ite
  * keep = [1,1]: pairs i<j of the F fields, logit = Σ_a p_a·relu(((e_i⊙e_j)·W)_a
  * + b_a), att = softmax over pairs, out = (Σ att·(e_i⊙e_j))·P + Σ w + w0.
  * Wt: device float [A][k] = attention_W TRANSPOSED; att_b [A], att_p [A],
- * P [k] (the prediction vector).  F <= 11, k % 4 == 0.
+ * P [k] (the prediction vector).  F <= 16, k % 4 == 0.
  * ---------------------------------------------------------------------- */
 int hhfm_afm_forward_workspace(int64_t B, int32_t F, int32_t A, size_t* ws_bytes);
 int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,

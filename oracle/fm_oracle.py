@@ -472,7 +472,7 @@ def afm_train_step(X, y, E, w, w0, W, b, pvec, P, acc, lr, lam, optimizer="adagr
 
     def upd(var, grad, key):
         if optimizer == "adagrad":
-            var, acc[key] = tf_adagrad(var, grad, acc[key], lr)
+            var, acc[key] = tf_adagrad(var, grad, acc[key].reshape(np.shape(var)), lr)
             return var
         return (var - F32(lr) * grad).astype(F32)
 

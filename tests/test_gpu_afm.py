@@ -88,6 +88,8 @@ def test_afm_catalog_query_chunks():
     (8, 64, 64, "bf16", 130),    # fused: 28 pairs (largest that fits 32 columns)
     (9, 32, 32, "f32", 300),     # GEMM path: 36 pairs > 32
     (5, 20, 16, "f32", 77),      # GEMM path: k % 8 != 0
+    (12, 64, 64, "f32", 203),    # GEMM path: 66 pairs (resturant / ml width, F = 12)
+    (16, 32, 48, "bf16", 65),    # GEMM path: 120 pairs, the largest F
 ])
 def test_afm_rows_envelope(F, k, A, tdt, B):
     """A1 across the fused kernel's envelope (F <= 8, k % 8 == 0) and the
@@ -118,6 +120,7 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     (9, 32, 32, "f32", 11, 500, 20),      # GEMM path: 8 query fields
     (5, 20, 16, "f32", 13, 400, 20),      # GEMM path: k % 8 != 0
     (5, 128, 128, "f32", 6, 300, 20),     # fused: 75 KB of LDS (raised dynamic limit)
+    (12, 64, 64, "f32", 7, 250, 20),      # GEMM path: 11 query fields (F = 12 datasets)
 ])
 def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
     """A2 across the fused kernel's envelope and the GEMM path beyond it."""
