@@ -745,11 +745,11 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
     int64_t tblocks = (nq + 3) / 4;
     if (tblocks > 4096) tblocks = 4096;
     if (K <= 32)
-      hipLaunchKernelGGL(topk_dense_kernel<32>, dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
+      hipLaunchKernelGGL((topk_dense_kernel<32, 32>), dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
                          item_count, (int64_t)item_count, K, global_item_base,
                          top_score + b0 * K, top_idx + b0 * K);
     else
-      hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
+      hipLaunchKernelGGL((topk_dense_kernel<64, 32>), dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
                          item_count, (int64_t)item_count, K, global_item_base,
                          top_score + b0 * K, top_idx + b0 * K);
   }

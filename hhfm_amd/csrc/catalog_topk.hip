@@ -113,7 +113,41 @@ HHFM_DEV void insert_one(float* ls, int32_t* li, float s, int32_t it, int K) {
   }
 }
 
-template <bool BF16, int KT, int KPAD, bool FM>
+// fp32 -> three bf16 pieces, x == p0 + p1 + p2 exactly for normal x: p0 =
+// RNE(x) takes the top 8 significant bits, x - p0 is exact (Sterbenz) and
+// keeps <= 16, the next piece 8 of those, the last piece the rest.
+HHFM_DEV uint32_t bf16x2_rne(float lo, float hi) {   // v_cvt_pk_bf16_f32
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  const bf16x2v v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+HHFM_DEV void split3x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  u32x4_t w0, w1, w2;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const float a = x[2 * v], b = x[2 * v + 1];
+    const uint32_t u0 = bf16x2_rne(a, b);
+    const float ra = a - __uint_as_float(u0 << 16), rb = b - __uint_as_float(u0 & 0xffff0000u);
+    const uint32_t u1 = bf16x2_rne(ra, rb);
+    const uint32_t u2 = bf16x2_rne(ra - __uint_as_float(u1 << 16),
+                                   rb - __uint_as_float(u1 & 0xffff0000u));
+    w0[v] = u0;
+    w1[v] = u1;
+    w2[v] = u2;
+  }
+  p0 = __builtin_bit_cast(bf16x8, w0);
+  p1 = __builtin_bit_cast(bf16x8, w1);
+  p2 = __builtin_bit_cast(bf16x8, w2);
+}
+
+// SPLIT: the dot products on v_mfma_f32_32x32x16_bf16 (16x the fp32 MFMA
+// rate) with every fp32 operand split into three bf16 pieces.  bf16 tables:
+// item·q = item·q0 + item·q1 + item·q2, every product exact in fp32 (3 MFMAs
+// per 16 k instead of 8 fp32 ones).  fp32 tables: the six piece products of
+// order >= 2^-16 (the dropped ones are < 2^-24 relative), 6 MFMAs per 16 k
+// instead of 8.  The result differs from the k-ordered fmaf chain only in
+// fp32 accumulation order (~1e-7 relative; tolerance 1e-5, north_star).
+template <bool BF16, int KT, int KPAD, bool FM, bool SPLIT>
 __global__ __launch_bounds__(256) void catalog_main(
     const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
     const char* __restrict__ E, int64_t item_row_begin, int32_t N,
@@ -166,6 +200,23 @@ __global__ __launch_bounds__(256) void catalog_main(
       bq[t][4 * v + 2] = x.z; bq[t][4 * v + 3] = x.w;
     }
   }
+  // split B operand: per 16-k MFMA step u, lane half h holds the query's k
+  // values of chunk u (bf16 tables) or of chunks 2u, 2u+1 (fp32 tables) —
+  // the same k the A operand's item values carry
+  constexpr int NU = SPLIT ? (BF16 ? KT : KT / 2) : 1;
+  bf16x8 qp[3][NU];
+  if constexpr (SPLIT) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if constexpr (BF16) x[e] = bq[u][e];
+        else x[e] = bq[2 * u + (e >> 2)][e & 3];
+      }
+      split3x8(x, qp[0][u], qp[1][u], qp[2][u]);
+    }
+  }
   float cq = 0.f;
   if constexpr (FM) cq = cst[q];
   float thr = (q < B) ? kNegInf : __builtin_huge_valf();
@@ -189,6 +240,40 @@ __global__ __launch_bounds__(256) void catalog_main(
     f32x16 acc = {0};
     const int nxt = tile + 1 < tb1 ? tile + 1 : tile;
     float wcur = wi;
+    auto refill = [&](int t) {   // rolling prefetch: chunk t of the next tile
+      int item = nxt * kTile + j;
+      item = item < N ? item : N - 1;
+      a[t] = *reinterpret_cast<const uint4*>(E + (item_row_begin + item) * ROWB + 16 * h + 32 * t);
+    };
+    if constexpr (SPLIT && BF16) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const bf16x8 ai = __builtin_bit_cast(bf16x8, a[t]);
+        refill(t);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[2][t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[1][t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[0][t], acc, 0, 0, 0);
+      }
+    } else if constexpr (SPLIT) {
+#pragma unroll
+      for (int u = 0; u < KT / 2; ++u) {
+        const float x[8] = {__uint_as_float(a[2 * u].x), __uint_as_float(a[2 * u].y),
+                            __uint_as_float(a[2 * u].z), __uint_as_float(a[2 * u].w),
+                            __uint_as_float(a[2 * u + 1].x), __uint_as_float(a[2 * u + 1].y),
+                            __uint_as_float(a[2 * u + 1].z), __uint_as_float(a[2 * u + 1].w)};
+        refill(2 * u);
+        refill(2 * u + 1);
+        bf16x8 i0, i1, i2;
+        split3x8(x, i0, i1, i2);
+        // smallest terms first
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, qp[0][u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[1][u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[2][u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[0][u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[1][u], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[0][u], acc, 0, 0, 0);
+      }
+    } else
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       float av[EPC];
@@ -311,6 +396,128 @@ __global__ __launch_bounds__(256) void catalog_main(
 }
 
 // ---------------------------------------------------------------------------
+// 2b. small catalogs (N <= 16,384, e.g. Frappe's 4,082 items): workgroup =
+// 16 waves = 16 queries x one item split.  Per chunk of up to 1,024 items the
+// waves score 16-item x 16-query tiles with v_mfma_f32_16x16x4_f32 (exact
+// fp32; A = item rows, lane group g taking the contiguous k-range
+// [g·k/4, (g+1)·k/4) so a lane's operand is one contiguous piece of its item
+// row; B = the queries' vectors, held in VGPRs for the whole kernel) and park
+// the 16 x 1,024 scores in LDS (one ds_write_b128 of 4 consecutive items per
+// lane and tile).  Then wave q folds query q's row of the chunk into its
+// running top-K list (topk_fold_chunk: lane-max bound, candidate compaction,
+// a bitonic sort sized to the candidates + merge).  The fold is a dependent
+// chain of cross-lane steps, so the workgroup is 16 waves (2 per CU fit:
+// 8 per SIMD) to keep the SIMDs issuing.  No [B, N] matrix touches HBM.
+// ---------------------------------------------------------------------------
+#ifndef HHFM_SMALL_KO
+#define HHFM_SMALL_KO 0   // diagnostic knock-outs: 1 = no selection, 2 = no scoring
+#endif
+constexpr int kSmallQ = 16;      // queries per workgroup (MFMA N) = waves per workgroup
+constexpr int kSmallCN = 1024;   // items per LDS chunk
+constexpr int kSmallLd = kSmallCN + 4;
+
+template <bool BF16, int KQ, int KPAD>
+__global__ __launch_bounds__(1024) void catalog_small(
+    const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
+    const char* __restrict__ E, int64_t item_row_begin, int32_t N,
+    const float* __restrict__ w, int fm, int K, int S, int items_per_split,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int64_t ostride_b,
+    int64_t ostride_s, int32_t gbase) {
+  constexpr int k = 4 * KQ;
+  constexpr int ESZ = BF16 ? 2 : 4;
+  constexpr int NW = kSmallQ;
+  __shared__ __attribute__((aligned(16))) float sc[kSmallQ * kSmallLd];
+  __shared__ float cand_s[NW][kWave];
+  __shared__ int32_t cand_i[NW][kWave];
+
+  const int qg = blockIdx.x / S, split = blockIdx.x - (blockIdx.x / S) * S;
+  const int wv = threadIdx.x >> 6, l = lane_id();
+  const int qj = l & 15, g = l >> 4;
+  const int64_t q0 = (int64_t)qg * kSmallQ;
+
+  // B operand: query q0 + qj, k-range [g·KQ, g·KQ + KQ)  (H is zero-padded to Bpad)
+  float hq[KQ];
+  {
+    const float4* src = reinterpret_cast<const float4*>(H + (q0 + qj) * k + g * KQ);
+#pragma unroll
+    for (int v = 0; v < KQ / 4; ++v) {
+      const float4 x = src[v];
+      hq[4 * v] = x.x; hq[4 * v + 1] = x.y; hq[4 * v + 2] = x.z; hq[4 * v + 3] = x.w;
+    }
+  }
+  const float cq = fm ? cst[q0 + qj] : 0.f;
+
+  // wave wv's running list: query q0 + wv
+  float ls = kNegInf, thr = kNegInf;
+  int32_t li = kNoIdx;
+  const int32_t i0 = split * items_per_split;
+  const int32_t i1 = min(N, i0 + items_per_split);
+
+  for (int32_t cb = i0; cb < i1; cb += kSmallCN) {
+    const int cn = min(kSmallCN, i1 - cb);
+    const int ntile = (cn + 15) >> 4;
+    constexpr int NR = KQ * ESZ / 16;
+    for (int t = wv; t < ntile && !(HHFM_SMALL_KO & 2); t += NW) {
+      int item = cb + t * 16 + qj;                  // A row of this lane
+      item = item < i1 ? item : i1 - 1;
+      const uint4* row = reinterpret_cast<const uint4*>(
+          E + (item_row_begin + item) * (int64_t)(k * ESZ) + g * KQ * ESZ);
+      uint4 raw[NR];
+#pragma unroll
+      for (int v = 0; v < NR; ++v) raw[v] = row[v];
+      float av[KQ];
+#pragma unroll
+      for (int v = 0; v < NR; ++v) {
+        const uint32_t r4[4] = {raw[v].x, raw[v].y, raw[v].z, raw[v].w};
+        if constexpr (BF16) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            av[8 * v + 2 * e] = __uint_as_float(r4[e] << 16);
+            av[8 * v + 2 * e + 1] = __uint_as_float(r4[e] & 0xffff0000u);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) av[4 * v + e] = __uint_as_float(r4[e]);
+        }
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < KQ; ++e)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], hq[e], acc, 0, 0, 0);
+      // acc[r] = score(item cb + 16 t + 4 g + r, query q0 + qj)
+      if (fm) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int it = cb + t * 16 + 4 * g + r;
+          const float wi = (w && it < i1) ? w[item_row_begin + it] : 0.f;
+          acc[r] = (acc[r] + wi) + cq;              // w_item, (u+f)·f   FM.py:178-184
+        }
+      }
+      *reinterpret_cast<f32x4*>(&sc[qj * kSmallLd + t * 16 + 4 * g]) = acc;
+    }
+    __syncthreads();
+    if (!(HHFM_SMALL_KO & 1)) {
+      const float* rowp = sc + wv * kSmallLd;
+      float v[kSmallCN / kWave];
+#pragma unroll
+      for (int j = 0; j < kSmallCN / kWave; ++j) {
+        const int x = j * kWave + l;
+        v[j] = x < cn ? rowp[x] : kNegInf;
+      }
+      topk_fold_chunk<KPAD, kSmallCN / kWave>(v, rowp, cb - i0, cn + (cb - i0), K, ls, li, thr,
+                                              cand_s[wv], cand_i[wv]);
+    }
+    __syncthreads();
+  }
+  // list indices are split-relative; emit global ids
+  const int64_t b = q0 + wv;
+  if (b < B && l < K) {
+    out_s[b * ostride_b + split * ostride_s + l] = ls;
+    out_i[b * ostride_b + split * ostride_s + l] = li == kNoIdx ? kNoIdx : li + i0 + gbase;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 3. merge of R sorted lists per query
 // ---------------------------------------------------------------------------
 template <int KPAD>
@@ -343,7 +550,9 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 struct Plan {
   int64_t Bpad;
   int nqb, S, tiles_per_split;
-  bool dense;            // small catalog: score matrix + dense top-K
+  bool small;            // small catalog, k in {32, 64, 128}: catalog_small
+  int Ss, ips;           //   its item splits and items per split
+  bool dense;            // small catalog, other k: score matrix + dense top-K
   int64_t ldsc;
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, total;
 };
@@ -359,6 +568,12 @@ static bool dense_catalog(int64_t B, int32_t N) {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+static bool small_catalog(int64_t B, int32_t N, int32_t k) {
+  const char* e = getenv("HHFM_CATALOG_SMALL");
+  if (!e || e[0] != '1') return false;   // opt-in: C3 0.12 ms vs 0.096 ms on the dense path
+  return dense_catalog(B, N) && (k == 32 || k == 64 || k == 128);
+}
+
 static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   Plan p{};
   p.nqb = (int)((B + kQPerBlock - 1) / kQPerBlock);
@@ -373,24 +588,41 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   if (S < 1) S = 1;
   p.tiles_per_split = (ntiles + S - 1) / S;
   p.S = (ntiles + p.tiles_per_split - 1) / p.tiles_per_split;
+  p.small = small_catalog(B, N, k);
+  p.dense = !p.small && dense_catalog(B, N);
+  if (p.small) {   // ~2 workgroups per CU; >= 256 items per split
+    const int nqg = (int)((B + kSmallQ - 1) / kSmallQ);
+    int ss = (512 + nqg - 1) / nqg;
+    const int smax = (N + 255) / 256;
+    ss = ss > smax ? smax : (ss < 1 ? 1 : ss);
+    p.ips = (((N + ss - 1) / ss) + 15) & ~15;
+    p.Ss = (N + p.ips - 1) / p.ips;
+  }
+  const int nsplit = p.small ? p.Ss : p.S;
   size_t off = 0;
   p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
   p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
   p.off_thr = off; off += align256((size_t)p.Bpad * sizeof(int32_t));
   p.off_ps = off;
-  if (p.S > 1) {
-    off += align256((size_t)B * p.S * K * sizeof(float));
+  if (nsplit > 1) {
+    off += align256((size_t)B * nsplit * K * sizeof(float));
     p.off_pi = off;
-    off += align256((size_t)B * p.S * K * sizeof(int32_t));
+    off += align256((size_t)B * nsplit * K * sizeof(int32_t));
   } else {
     p.off_pi = off;
   }
-  p.dense = dense_catalog(B, N);
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
   if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
   p.total = off;
   return p;
+}
+
+// HHFM_CATALOG_EXACT=1 selects the fp32-MFMA (k-ordered fmaf chain) kernel
+// instead of the split-bf16 one (A/B and numerics comparisons).
+static bool catalog_exact() {
+  const char* e = getenv("HHFM_CATALOG_EXACT");
+  return e && e[0] == '1';
 }
 
 template <bool BF16, int KT, int KPAD, bool FM>
@@ -399,9 +631,15 @@ static void launch_main(const Plan& p, const float* H, const float* cst, int64_t
                         const float* w, int K, float* os, int32_t* oi,
                         int64_t sb, int64_t ss, int32_t gbase, int32_t* gthr,
                         hipStream_t st) {
-  hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM>), dim3(p.nqb * p.S),
-                     dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
-                     p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
+  constexpr bool kCanSplit = BF16 || KT >= 2;   // fp32 split steps pair two chunks
+  if (kCanSplit && !catalog_exact())
+    hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM, kCanSplit>), dim3(p.nqb * p.S),
+                       dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
+                       p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
+  else
+    hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM, false>), dim3(p.nqb * p.S),
+                       dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
+                       p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
 }
 
 template <bool BF16, int KPAD, bool FM>
@@ -498,6 +736,35 @@ extern "C" int hhfm_catalog_topk(
       hipLaunchKernelGGL(catalog_queries<false>, dim3((int)blocks), dim3(256), 0, st,
                          qidx, B, p.Bpad, ncols, mode, user_col, ctx_begin,
                          ctx_end, time_begin, time_end, Eb, features_M, k, H, cst);
+  }
+
+  if (p.small) {
+    const bool fmm = mode == HHFM_MODE_FM;
+    const int nqg = (int)((B + kSmallQ - 1) / kSmallQ);
+    float* os = p.Ss > 1 ? reinterpret_cast<float*>(ws + p.off_ps) : top_score;
+    int32_t* oi = p.Ss > 1 ? reinterpret_cast<int32_t*>(ws + p.off_pi) : top_idx;
+    const int64_t sb = p.Ss > 1 ? (int64_t)p.Ss * K : K, ss = p.Ss > 1 ? K : 0;
+#define HHFM_SMALL(BF, KQ, KP)                                                                \
+  hipLaunchKernelGGL((catalog_small<BF, KQ, KP>), dim3(nqg * p.Ss), dim3(1024), 0, st, H, cst, \
+                     B, Eb, (int64_t)item_row_begin, item_count, fmm ? w : nullptr, (int)fmm,  \
+                     K, p.Ss, p.ips, os, oi, sb, ss, global_item_base)
+#define HHFM_SMALL_KQ(BF, KP)                    \
+  switch (k) {                                   \
+    case 32: HHFM_SMALL(BF, 8, KP); break;       \
+    case 64: HHFM_SMALL(BF, 16, KP); break;      \
+    default: HHFM_SMALL(BF, 32, KP); break;      \
+  }
+    if (K <= 32) {
+      if (bf16) { HHFM_SMALL_KQ(true, 32) } else { HHFM_SMALL_KQ(false, 32) }
+    } else {
+      if (bf16) { HHFM_SMALL_KQ(true, 64) } else { HHFM_SMALL_KQ(false, 64) }
+    }
+#undef HHFM_SMALL_KQ
+#undef HHFM_SMALL
+    if (p.Ss > 1)
+      launch_merge(os, oi, p.Ss, B, K, /*stride_r=*/K, /*stride_b=*/(int64_t)p.Ss * K,
+                   top_score, top_idx, st);
+    return (int)hipGetLastError();
   }
 
   if (p.dense) {

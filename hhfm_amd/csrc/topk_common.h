@@ -6,6 +6,13 @@
 #pragma once
 #include "hhfm_common.h"
 
+#ifndef HHFM_TOPK_NV
+#define HHFM_TOPK_NV 32   // scores per lane per chunk in topk_dense
+#endif
+#ifndef HHFM_TOPK_NT
+#define HHFM_TOPK_NT 1    // non-temporal score loads in topk_dense
+#endif
+
 namespace hhfm {
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -100,14 +107,101 @@ HHFM_DEV void merge_lists(float& as, int32_t& ai, float bs, int32_t bi) {
 
 // ---------------------------------------------------------------------------
 // dense top-K over materialised scores [B][N] (wave per query)
+//
+// The row is read in chunks of NV·64 scores, all NV loads of a lane issued
+// before any is used (one memory latency per chunk, not one per 64 scores).
+// Before filtering a chunk, the threshold is raised to the K-th best of the
+// chunk's 64 lane maxima: K distinct lanes each hold a score at least that
+// large, so it never exceeds the row's K-th best score and every top-K
+// candidate still passes `s >= thr` — while nearly all others fail.  The
+// chunk's candidates (typically 20–40) are compacted through LDS (ballot +
+// mbcnt positions) into one register per lane, sorted by one 64-lane bitonic
+// network and merged into the list in one step.  More than 64 candidates
+// (heavy ties) fall back to per-64-score filtering.
 // ---------------------------------------------------------------------------
-template <int KPAD>
+// Fold one chunk of NV·64 scores (lane l holds v[j] = score of index
+// cb + 64 j + l = src[64 j + l]; indices >= n are ignored) into the wave's
+// running top-K list (ls, li: lanes [0, KPAD), sorted) with threshold thr.
+// cs / ci: 64 LDS slots private to the wave.  The rare heavy-tie path
+// re-reads src in a rolled loop (keeps the kernel's code small: a fully
+// unrolled fallback made these kernels instruction-fetch bound).
+template <int KPAD, int NV>
+HHFM_DEV void topk_fold_chunk(const float (&v)[NV], const float* src, int32_t cb, int32_t n,
+                              int K, float& ls, int32_t& li, float& thr, float* cs_lds,
+                              int32_t* ci_lds) {
+  const int l = lane_id();
+  if (thr == kNegInf) {   // list not full yet: K-th best lane maximum bounds the K-th score
+    float mx = v[0];
+#pragma unroll
+    for (int j = 1; j < NV; ++j) mx = fmaxf(mx, cb + j * kWave + l < n ? v[j] : kNegInf);
+    if (cb + l >= n) mx = kNegInf;
+    int32_t dummy = l;
+    bitonic_sort_desc<64>(mx, dummy);
+    thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), K - 1));
+  }
+  // cheap test first: most chunks after the first hold few or no candidates
+  int mine = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) mine += (cb + j * kWave + l < n && v[j] >= thr) ? 1 : 0;
+  if (__ballot(mine > 0) == 0) return;
+  int total = 0;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int32_t i = cb + j * kWave + l;
+    const bool pass = i < n && v[j] >= thr;
+    const uint64_t m = __ballot(pass);
+    if (pass) {
+      const int pos = total + (int)__builtin_amdgcn_mbcnt_hi(
+                                  (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (pos < kWave) {
+        cs_lds[pos] = v[j];
+        ci_lds[pos] = i;
+      }
+    }
+    total += __popcll(m);
+  }
+  if (total <= kWave) {
+    __builtin_amdgcn_wave_barrier();
+    float cs = l < total ? cs_lds[l] : kNegInf;
+    int32_t ci = l < total ? ci_lds[l] : kNoIdx;
+    __builtin_amdgcn_wave_barrier();   // the next chunk rewrites the slots
+    // the smallest network that covers the candidates (lanes >= total hold -inf,
+    // so the whole 64-lane sequence is sorted once the first group is)
+    if (total <= 2) bitonic_sort_desc<2>(cs, ci);
+    else if (total <= 4) bitonic_sort_desc<4>(cs, ci);
+    else if (total <= 8) bitonic_sort_desc<8>(cs, ci);
+    else if (total <= 16) bitonic_sort_desc<16>(cs, ci);
+    else if (total <= 32) bitonic_sort_desc<32>(cs, ci);
+    else bitonic_sort_desc<64>(cs, ci);
+    merge_lists<KPAD>(ls, li, cs, ci);
+  } else {   // heavy ties: filter 64 scores at a time
+#pragma unroll 1
+    for (int j = 0; j < NV; ++j) {
+      const int32_t i = cb + j * kWave + l;
+      const float x = i < n ? src[j * kWave + l] : kNegInf;
+      const bool pass = i < n && x >= thr;
+      if (__ballot(pass) == 0) continue;
+      float cs = pass ? x : kNegInf;
+      int32_t ci = pass ? i : kNoIdx;
+      bitonic_sort_desc<64>(cs, ci);
+      merge_lists<KPAD>(ls, li, cs, ci);
+      if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
+      thr = fmaxf(thr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1)));
+    }
+  }
+  if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
+  thr = fmaxf(thr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1)));
+}
+
+template <int KPAD, int NV>
 __global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict__ S,
                                                          int64_t B, int32_t N, int64_t lds,
                                                          int K, int32_t base,
                                                          float* __restrict__ out_s,
                                                          int32_t* __restrict__ out_i) {
-  const int l = lane_id();
+  __shared__ float cand_s[4][kWave];
+  __shared__ int32_t cand_i[4][kWave];
+  const int l = lane_id(), wv = (threadIdx.x >> 6) & 3;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
   const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
   for (int64_t b = wave; b < B; b += nwave) {
@@ -115,36 +209,14 @@ __global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict
     float ls = kNegInf;
     int32_t li = kNoIdx;
     float thr = kNegInf;
-    for (int32_t c0 = 0; c0 < N; c0 += kWave) {
-      const int32_t i = c0 + l;
-      const float s = i < N ? row[i] : kNegInf;
-      const bool pass = i < N && s >= thr;
-      const uint64_t m = __ballot(pass);
-      const int cnt = __popcll(m);
-      if (cnt == 0) continue;
-      if (cnt > 8) {
-        float cs = pass ? s : kNegInf;
-        int32_t ci = pass ? i : kNoIdx;
-        bitonic_sort_desc<64>(cs, ci);
-        merge_lists<KPAD>(ls, li, cs, ci);
-      } else {
-        uint64_t mm = m;
-        while (mm) {
-          const int L = __builtin_ctzll(mm);
-          mm &= mm - 1;
-          const float sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), L));
-          const int32_t ic = c0 + L;
-          const int pos = __popcll(__ballot(l < KPAD && better(ls, li, sc, ic)));
-          if (pos < K) {
-            const float ps = __shfl_up(ls, 1, kWave);
-            const int32_t pi = __shfl_up(li, 1, kWave);
-            if (l > pos) { ls = ps; li = pi; }
-            else if (l == pos) { ls = sc; li = ic; }
-          }
-        }
+    for (int32_t cb = 0; cb < N; cb += NV * kWave) {
+      float v[NV];
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        const int32_t i = cb + j * kWave + l;
+        v[j] = i < N ? (HHFM_TOPK_NT ? __builtin_nontemporal_load(row + i) : row[i]) : kNegInf;
       }
-      if (l >= KPAD) { ls = kNegInf; li = kNoIdx; }
-      thr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1));
+      topk_fold_chunk<KPAD, NV>(v, row + cb, cb, N, K, ls, li, thr, cand_s[wv], cand_i[wv]);
     }
     if (l < K) {
       out_s[b * K + l] = ls;
@@ -159,10 +231,10 @@ static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
   if (K <= 32)
-    hipLaunchKernelGGL(topk_dense_kernel<32>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+    hipLaunchKernelGGL((topk_dense_kernel<32, HHFM_TOPK_NV>), dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
                        K, base, os, oi);
   else
-    hipLaunchKernelGGL(topk_dense_kernel<64>, dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
+    hipLaunchKernelGGL((topk_dense_kernel<64, HHFM_TOPK_NV>), dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
                        K, base, os, oi);
 }
 

@@ -78,6 +78,14 @@ if not only or "k2" in only:
                      "pairs_per_s": B * ni / (med * 1e-3)}
         del E
         torch.cuda.empty_cache()
+if "topk" in only:   # dense top-K alone (C3 score-matrix shape), diagnostic leg
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    for name, B, N in [("topk_dense_3000x4082", 3000, 4082), ("topk_dense_300x4082", 300, 4082),
+                       ("topk_dense_60x4082", 60, 4082)]:
+        S = torch.randn(B, N, generator=g, device=dev) * 0.01
+        med, mn = timeit(lambda: ops.topk_dense(S, 20), reps=20)
+        res[name] = {"median_ms": med, "min_ms": mn}
 if not only or "dfm" in only:
     # C5 per-GPU shape (DFM k=256, 3x400 MLP, Frappe-field rows), 2 M rows per launch
     from hhfm_amd.DFM import DeepFM

@@ -249,4 +249,57 @@ if not only or "h6" in only:
         "unit": "steps/s", "gpu_ms_wall": ms, "gpu_rate": 1e3 / ms,
         "cpu_rate_numpy": 1.0 / c, "cpu_sample": "same batch, numpy oracle step"}
 
+
+def _train_row(step, cpu_step, reps=20):
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    return ms, cpu_s(cpu_step)
+
+
+# ---- H6: AFM / DeepFM training steps (main.py's factor 128, batch 5000, Frappe) ----
+if not only or "h6" in only:
+    from hhfm_amd.AFM import AFM
+    from hhfm_amd.DFM import DeepFM
+    from hhfm_amd import training
+    rng = np.random.default_rng(7)
+    X, M = frappe_rows(rng, 5000)
+    y = rng.choice([1.0, -1.0], 5000).astype(np.float32)[:, None]
+    m = AFM(957, 4082, M, 1, [128, 128], None, 0.1, 100.0, [1, 1], "AdagradOptimizer", 0.999, 5,
+            device=dev)
+    W = m.get_weights()
+    names = ["feature_embeddings", "feature_bias", "bias", "attention_W", "attention_b",
+             "attention_p", "prediction"]
+    cur = [np.asarray(W[n], np.float32) for n in names]
+    acc = {kk: np.full_like(v, 0.1) for kk, v in zip(["E", "w", "w0", "W", "b", "p", "P"], cur)}
+    ms, c = _train_row(lambda: training.afm_partial_fit(m, {"X": X, "Y": y}),
+                       lambda: orc.afm_train_step(X, y, *cur, acc, 0.1, 100.0))
+    res["H6_afm_train_step"] = {
+        "config": "AFM k=A=128 partial_fit, batch 5000 rows, Frappe vocab (F=5)",
+        "unit": "steps/s", "gpu_ms_wall": ms, "gpu_rate": 1e3 / ms,
+        "cpu_rate_numpy": 1.0 / c, "cpu_sample": "same batch, numpy oracle step"}
+    del m
+    m = DeepFM(957, 4082, M, 5, 128, [150, 200, 150], None, 0.01, 0, 0.01, device=dev)
+    W = m.get_weights()
+    L = 3
+    Ls = [W[f"layer_{i}"] for i in range(L)]
+    bs = [W[f"bias_{i}"][0] for i in range(L)]
+    keys = ["E", "w"] + [f"W{i}" for i in range(L)] + [f"b{i}" for i in range(L)] + ["Wp", "bp"]
+    vals = ([W["feature_embeddings"], W["feature_bias"][:, 0]] + Ls + bs
+            + [W["concat_projection"][:, 0], np.float32(W["concat_bias"])])
+    acc = {kk: np.full_like(np.asarray(v, np.float32), 0.1) for kk, v in zip(keys, vals)}
+    ms, c = _train_row(lambda: training.dfm_partial_fit(m, {"X": X, "Y": y}),
+                       lambda: orc.dfm_train_step(X, y, vals[0], vals[1], Ls, bs, vals[-2],
+                                                  vals[-1], acc, 0.01, 0.01))
+    res["H6_dfm_train_step"] = {
+        "config": "DeepFM k=128, MLP 150/200/150 partial_fit, batch 5000 rows, Frappe vocab",
+        "unit": "steps/s", "gpu_ms_wall": ms, "gpu_rate": 1e3 / ms,
+        "cpu_rate_numpy": 1.0 / c, "cpu_sample": "same batch, numpy oracle step"}
+    del m
+    torch.cuda.empty_cache()
+
 print(json.dumps(res, indent=1))

@@ -175,13 +175,17 @@ def test_catalog_topk_fm_parity(dtype, k):
     _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
 
 
+@pytest.mark.parametrize("exact", ["0", "1"])
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("k,K", [(32, 1), (128, 20), (64, 64)])
-def test_catalog_topk_streaming_path(mode, dtype, k, K):
+@pytest.mark.parametrize("k,K", [(16, 5), (32, 1), (128, 20), (64, 64)])
+def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
     """Catalogs above the small-catalog bound (N > 16384) take the streaming
-    threshold kernel; the 4082-item cases above take the dense score matrix."""
+    threshold kernel (split-bf16 MFMA by default, the fp32-MFMA fmaf chain
+    with HHFM_CATALOG_EXACT=1); the 4082-item cases above take the dense
+    score matrix."""
     from hhfm_amd import ops
+    monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
     rng = np.random.default_rng(17 + k + K)
     n_user, n_item = 300, 20000
     A, M = synth_rows(rng, 70, n_user, n_item, (7, 2, 3))
@@ -204,6 +208,34 @@ def test_catalog_topk_streaming_path(mode, dtype, k, K):
         it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
         scale = (q @ it.T + (q * np.abs(f)).sum(1, keepdims=True)).max(1, keepdims=True) + 0.05
     _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale)
+
+
+@pytest.mark.parametrize("mode", ["hhfm", "fm"])
+@pytest.mark.parametrize("small", ["1", "0"])
+def test_catalog_topk_small_path_ragged_shard(mode, small, monkeypatch):
+    """Small-catalog kernel (opt-in, HHFM_CATALOG_SMALL=1) and the default
+    GEMM + dense top-K path on a ragged shard: N % 16 != 0, non-zero row and global
+    bases, B % 16 != 0, item splits + merge."""
+    from hhfm_amd import ops
+    monkeypatch.setenv("HHFM_CATALOG_SMALL", small)
+    rng = np.random.default_rng(23)
+    n_user, n_item, k = 400, 5000, 64
+    A, M = synth_rows(rng, 37, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    w = rng.normal(0, 0.01, size=M).astype(np.float32)
+    lo, cnt, gbase = n_user + 777, 1001, 777
+    m = ops.MODE_HHFM if mode == "hhfm" else ops.MODE_FM
+    s, i = ops.catalog_topk(_dev(A), _dev(E), m, 20, lo, cnt, gbase,
+                            _dev(w) if mode == "fm" else None, 0, (2, 5), (0, 0))
+    if mode == "hhfm":
+        full = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
+        scale = _hhfm_scale(A, E, n_user, n_item)
+    else:
+        full = orc.fm_catalog_scores(A, E, w, n_user, n_item)
+        scale = np.abs(full).max(1, keepdims=True) + 0.05
+    ref = np.full_like(full, -np.inf)
+    ref[:, gbase:gbase + cnt] = full[:, gbase:gbase + cnt]
+    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
 
 
 def test_catalog_topk_large_catalog_shard_offsets():
