@@ -108,6 +108,32 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_catalog_topk");
         });
 
+  m.def("pf_contains",
+        [](uptr keys, int64_t nkeys, int key_cols, uptr codes, int64_t ncodes, uptr rows,
+           int64_t B, int ncols, int item_col, uptr cand, int num, uptr out, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_pf_contains(P<const int32_t>(keys), nkeys, key_cols, P<const int64_t>(codes),
+                                  ncodes, P<const int32_t>(rows), B, ncols, item_col,
+                                  P<const int32_t>(cand), num, P<uint8_t>(out), P<void>(stream));
+          }
+          check(rc, "hhfm_pf_contains");
+        });
+
+  m.def("topk_walk",
+        [](uptr pred, int64_t B, int Pn, uptr target, uptr positive, int TopK, uptr outcome,
+           uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_topk_walk(P<const int32_t>(pred), B, Pn, P<const int32_t>(target),
+                                P<const uint8_t>(positive), TopK, P<int32_t>(outcome),
+                                P<void>(stream));
+          }
+          check(rc, "hhfm_topk_walk");
+        });
+
   m.def("topk_merge",
         [](uptr in_score, uptr in_idx, int R, int64_t B, int K, uptr out_score,
            uptr out_idx, uptr stream) {

@@ -19,6 +19,15 @@ H3-H5, Appendix 3-4, 6), because HR parity depends on them:
 The model is duck-typed: ``model.score_rows(X) -> float32 [B,1]`` (replaces
 ``sess.run(model.out | model.PositiveFeadback)``) and
 ``model.topk(A, tp) -> int [B,tp]`` item offsets.
+
+With a model on the GPU (``model.device`` a cuda device) the per-element
+work runs on the device: the rejection test of
+``sample_negative`` and evaluate_TopK's target test through
+``hhfm_pf_contains`` (positive_feedback as sorted key / (key, item) code
+arrays, ``DevicePairSet``), the metric walk through ``hhfm_topk_walk``.
+The random draws stay on the host (numpy's stream) and the walk's ranks are
+turned into the reference's float64 values on the host, so the results are
+identical to the host path (tests/test_gpu_harness.py).
 """
 from __future__ import annotations
 
@@ -54,6 +63,41 @@ class _PairSet:
         return hit
 
 
+class DevicePairSet:
+    """positive_feedback as the two sorted device arrays hhfm_pf_contains
+    searches: distinct keys [nkeys, key_cols] int32 in lexicographic order,
+    and (key rank << 32 | item) int64 codes, sorted."""
+
+    def __init__(self, positive_feedback, key_cols, device):
+        import torch
+        keys = list(positive_feedback.keys())
+        K = np.asarray(keys, dtype=np.int64).reshape(len(keys), key_cols)
+        order = np.lexsort(K.T[::-1]) if len(keys) else np.zeros(0, np.int64)
+        lens = np.fromiter((len(positive_feedback[keys[i]]) for i in order), dtype=np.int64,
+                           count=len(order))
+        items = np.fromiter((it for i in order for it in positive_feedback[keys[i]]),
+                            dtype=np.int64, count=int(lens.sum()))
+        codes = np.sort((np.repeat(np.arange(len(order), dtype=np.int64), lens) << 32) | items)
+        self.key_cols = key_cols
+        self.n = len(keys)
+        self.keys = torch.from_numpy(np.ascontiguousarray(K[order], dtype=np.int32)).to(device)
+        self.codes = torch.from_numpy(codes).to(device)
+        self.device = device
+
+    def contains(self, rows, cand=None):
+        """rows int [B, key_cols+1] (item in column 1); cand int [B, num] or
+        None (the rows' own items) -> numpy bool [B, num] / [B]."""
+        import torch
+        from . import ops
+        B = len(rows)
+        if self.n == 0 or B == 0:
+            return np.zeros((B,) if cand is None else (B, np.shape(cand)[1]), dtype=bool)
+        r = torch.from_numpy(np.ascontiguousarray(rows, dtype=np.int32)).to(self.device)
+        c = None if cand is None else \
+            torch.from_numpy(np.ascontiguousarray(cand, dtype=np.int32)).to(self.device)
+        return ops.pf_contains(self.keys, self.codes, r, 1, c).cpu().numpy().astype(bool)
+
+
 def row_keys(data):
     """tuple(user[[i for i in range(len(user)) if i != 1]]) per row
     (FM.py:291): every column except the item."""
@@ -85,6 +129,7 @@ class Train(object):
         self.model = model
         self._pairs = None
         self._pairs_src = None
+        self._dpairs = None
 
     # -- H5 -----------------------------------------------------------------
     def _pair_index(self):
@@ -96,14 +141,43 @@ class Train(object):
             self._pairs_n = sum(len(v) for v in pf.values())
         return self._pairs
 
+    def _device(self):
+        """The model's cuda device, or None (host harness)."""
+        dev = getattr(self.model, "device", None)
+        if dev is None:
+            return None
+        import torch
+        dev = torch.device(dev)
+        return dev if dev.type == "cuda" else None
+
+    def _device_pairs(self, dev, key_cols):
+        pf = self.data.positive_feedback
+        n = sum(len(v) for v in pf.values())
+        d = self._dpairs
+        if d is None or d[0] is not pf or d[1] != n or d[2].device != dev or \
+                d[2].key_cols != key_cols:
+            self._dpairs = d = (pf, n, DevicePairSet(pf, key_cols, dev))
+        return d[2]
+
     def sample_negative(self, data, num=10):
         """FM.py:284-294 with the same np.random stream."""
         lo, hi = self.n_user, self.n_user + self.n_item
         samples = np.random.randint(lo, hi, size=(len(data), num))
         if len(data) == 0:
             return samples
-        keys = row_keys(data)
         pf = self.data.positive_feedback
+        dev = self._device()
+        if dev is not None:
+            data = np.asarray(data)
+            bad = self._device_pairs(dev, data.shape[1] - 1).contains(data, samples)
+            kcols = [c for c in range(data.shape[1]) if c != 1]
+            for i, j in np.argwhere(bad):      # row-major, like the nested loop
+                key = tuple(data[i, kcols].tolist())
+                neg = samples[i, j]
+                while neg in pf[key]:
+                    samples[i, j] = neg = np.random.randint(lo, hi)
+            return samples
+        keys = row_keys(data)
         bad = self._pair_index().contains(keys, samples)
         for i, j in np.argwhere(bad):      # row-major, like the nested loop
             key = keys[i]
@@ -139,9 +213,19 @@ class Train(object):
         dat = data1.values
         num = self.eval_num
         pf = self.data.positive_feedback
+        dev = self._device()
         for _ in range(int(size / num)):
             feed = np.array(dat[:, 1:][np.random.randint(0, len(dat), num)], dtype=np.int64)
             prediction = np.asarray(self.model.topk(feed, 20)) + self.n_user
+            if dev is not None:
+                for n in self._device_walk(dev, feed, prediction).tolist():
+                    if n >= 0:
+                        hits.append(1)
+                        ndcg.append(np.log(2) / np.log(n + 2))
+                        pre.append(1 / (n + 1))
+                    elif n == -1:
+                        hits.append(0); ndcg.append(0); pre.append(0)
+                continue
             for i, line in enumerate(feed):
                 item = line[1]
                 key = tuple(line[[c for c in range(len(line)) if c != 1]])
@@ -161,6 +245,21 @@ class Train(object):
                     else:
                         n = n + 1
         return [np.average(hits), np.average(ndcg), np.average(pre)]
+
+    def _device_walk(self, dev, feed, prediction):
+        """hhfm_pf_contains (target test) + hhfm_topk_walk for one batch ->
+        numpy int32 outcomes (see ops.topk_walk)."""
+        import torch
+        from . import ops
+        pairs = self._device_pairs(dev, feed.shape[1] - 1)
+        rows = torch.from_numpy(np.ascontiguousarray(feed, dtype=np.int32)).to(dev)
+        if pairs.n:
+            positive = ops.pf_contains(pairs.keys, pairs.codes, rows, 1)
+        else:
+            positive = torch.zeros(len(feed), dtype=torch.uint8, device=dev)
+        pred = torch.from_numpy(np.ascontiguousarray(prediction, dtype=np.int32)).to(dev)
+        target = rows[:, 1].contiguous()
+        return ops.topk_walk(pred, target, positive, self.TopK).cpu().numpy()
 
     def _log(self, line):
         print(line)

@@ -282,3 +282,40 @@ def afm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt: t
                          top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), ws.numel(),
                          _stream(dev))
     return top_s, top_i
+
+
+# ---- H5 / H3: harness membership test and metric walk ------------------------
+def pf_contains(keys: torch.Tensor, codes: torch.Tensor, rows: torch.Tensor, item_col: int,
+                cand: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """positive_feedback membership on the device (hhfm_pf_contains).
+
+    keys int32 [nkeys, ncols-1] (sorted, distinct), codes int64 (sorted),
+    rows int32 [B, ncols]; cand int32 [B, num] -> uint8 [B, num], or the
+    rows' own items (cand None) -> uint8 [B]."""
+    _need_cuda(keys, codes, rows, cand)
+    if keys.dtype != torch.int32 or codes.dtype != torch.int64 or rows.dtype != torch.int32:
+        raise TypeError("keys int32, codes int64, rows int32")
+    B, ncols = rows.shape
+    num = 1 if cand is None else cand.shape[1]
+    if cand is not None and (cand.dtype != torch.int32 or cand.shape[0] != B):
+        raise ValueError("cand must be int32 [B, num]")
+    out = torch.empty(B, num, dtype=torch.uint8, device=rows.device)
+    native().pf_contains(keys.data_ptr(), keys.shape[0], ncols - 1, codes.data_ptr(),
+                         codes.numel(), rows.data_ptr(), B, ncols, item_col,
+                         0 if cand is None else cand.data_ptr(), num, out.data_ptr(),
+                         _stream(rows.device))
+    return out if cand is not None else out[:, 0]
+
+
+def topk_walk(pred: torch.Tensor, target: torch.Tensor, positive: torch.Tensor,
+              TopK: int) -> torch.Tensor:
+    """evaluate_TopK's walk (hhfm_topk_walk): int32 [B] outcomes, n >= 0 hit
+    at walk position n, -1 miss (zeros appended), -2 nothing appended."""
+    _need_cuda(pred, target, positive)
+    if pred.dtype != torch.int32 or target.dtype != torch.int32 or positive.dtype != torch.uint8:
+        raise TypeError("pred/target int32, positive uint8")
+    B, P = pred.shape
+    out = torch.empty(B, dtype=torch.int32, device=pred.device)
+    native().topk_walk(pred.data_ptr(), B, P, target.data_ptr(), positive.data_ptr(), TopK,
+                       out.data_ptr(), _stream(pred.device))
+    return out

@@ -266,6 +266,33 @@ int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32
                     int32_t global_item_base, float* top_score, int32_t* top_idx,
                     void* stream);
 
+/* ------------------------------------------------------------------------
+ * H5 / H3 — harness membership test and metric walk
+ *
+ * positive_feedback (NewLoadData.py:49-56: key = every column but the item
+ * -> set of items) as two sorted device arrays: keys [nkeys][key_cols]
+ * int32, distinct, lexicographically sorted (key_cols = ncols - 1); codes
+ * [ncodes] int64 = (rank of the key in `keys`) << 32 | item, sorted.
+ *
+ * hhfm_pf_contains: out[b][j] = 1 iff cand[b][j] is in positive_feedback
+ * of row b's key — the rejection test of Train.sample_negative
+ * (FM.py:291-293).  cand == NULL (num = 1): the row's own item (column
+ * item_col) — evaluate_TopK's `item in positive_feedback[key]`
+ * (FM.py:343-355).  rows: int32 [B][ncols]; out: uint8 [B][num].
+ *
+ * hhfm_topk_walk: evaluate_TopK's walk over P predictions (FM.py:344-357)
+ * per row: outcome = n >= 0 (target at walk position n < TopK), -1 (walk
+ * passed TopK-1: the reference appends 0, 0, 0), -2 (predictions
+ * exhausted: it appends nothing).  pred: int32 [B][P] global item ids,
+ * target int32 [B], positive uint8 [B] (from hhfm_pf_contains).
+ * ---------------------------------------------------------------------- */
+int hhfm_pf_contains(const int32_t* keys, int64_t nkeys, int32_t key_cols,
+                     const int64_t* codes, int64_t ncodes, const int32_t* rows,
+                     int64_t B, int32_t ncols, int32_t item_col,
+                     const int32_t* cand, int32_t num, uint8_t* out, void* stream);
+int hhfm_topk_walk(const int32_t* pred, int64_t B, int32_t P, const int32_t* target,
+                   const uint8_t* positive, int32_t TopK, int32_t* outcome, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
