@@ -113,7 +113,7 @@ def test_topk_walk_matches_host_walk(TopK):
 
 
 def test_sample_negative_device_equals_host_at_frappe_shape(tmp_path):
-    """88k-row loader split, 50 negatives per row (evaluate_AUC's shape):
+    """A 30k-row Frappe-shape loader split, 50 negatives per row (evaluate_AUC):
     the device rejection test gives the host's samples exactly."""
     import bench
     from hhfm_amd.NewLoadData import LoadData
