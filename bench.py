@@ -47,9 +47,10 @@ def parse():
                    help="CPU-baseline time budget (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 21)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
-    p.add_argument("--legs", default="hr,catalog",
+    p.add_argument("--legs", default="hr,catalog,catalog_bf16",
                    help="extra legs: hr (HR@10 identity after GPU training on Frappe-shape "
-                        "data), catalog (C4 item-sharded top-K, RCCL all-gather at N>1)")
+                        "data), catalog / catalog_bf16 (C4 item-sharded top-K over an fp32 / "
+                        "bf16 table, RCCL all-gather at N>1)")
     p.add_argument("--hr-epochs", type=int, default=5)
     return p.parse_args()
 
@@ -177,10 +178,10 @@ def hr_leg(dev, epochs):
             "epoch_loss": losses, "train_s": t_train}
 
 
-def catalog_leg(dev, world, rank, reps=5):
+def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
     """C4: HHFM k=128, 1 M users, 10 M items sharded contiguously over the
-    ranks, 1,024 queries, K=20, fp32; local hhfm_catalog_topk + RCCL
-    all-gather + hhfm_topk_merge per step."""
+    ranks, 1,024 queries, K=20, fp32 (or bf16) table; local
+    hhfm_catalog_topk + RCCL all-gather + hhfm_topk_merge per step."""
     from hhfm_amd import distributed as hd
     from hhfm_amd import ops
     nu, ni, k, B, K = 1 << 20, 10_000_000, 128, 1024, 20
@@ -193,7 +194,7 @@ def catalog_leg(dev, world, rank, reps=5):
     gi = torch.Generator(device=dev)
     gi.manual_seed(1000 + rank)
     rows_item = torch.empty(end - begin, k, device=dev).normal_(0, 0.01, generator=gi)
-    E = torch.cat([rows_user, rows_item, rows_ctx]).contiguous()
+    E = torch.cat([rows_user, rows_item, rows_ctx]).to(table_dtype).contiguous()
     del rows_user, rows_item
     off = nu + (end - begin)
     cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
@@ -224,8 +225,10 @@ def catalog_leg(dev, world, rank, reps=5):
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
     ms = float(el[0]) / reps * 1e3
     pairs = B * ni
-    return {"workload": "C4: HHFM k=128 fp32, 10M-item catalog sharded over ranks, "
-                        "1,024 queries, top-20 (local MFMA score+select, RCCL all-gather, merge)",
+    tname = "fp32" if table_dtype == torch.float32 else "bf16"
+    return {"workload": f"C4: HHFM k=128 {tname} table, 10M-item catalog sharded over ranks, "
+                        "1,024 queries, top-20 (local split-bf16 MFMA score + select, RCCL "
+                        "all-gather, merge)",
             "ms_per_query_batch": ms, "pairs_per_s": pairs / (ms * 1e-3),
             "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world}
 
@@ -320,6 +323,12 @@ def main():
             extra["catalog_c4"] = catalog_leg(dev, world, rank)
         except Exception as e:  # noqa: BLE001
             extra["catalog_c4"] = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+    if "catalog_bf16" in legs:
+        try:
+            extra["catalog_c4_bf16"] = catalog_leg(dev, world, rank, table_dtype=torch.bfloat16)
+        except Exception as e:  # noqa: BLE001
+            extra["catalog_c4_bf16"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
     if "hr" in legs and rank == 0:
         try:

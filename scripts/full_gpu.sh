@@ -15,7 +15,7 @@ timeout -k 10 400 python bench.py > $out/bench.json 2> $out/bench.err || { echo 
 cat $out/bench.json
 bash scripts/gpu_profile.sh > $out/profile.log 2>&1 || { echo "profile failed"; tail $out/profile.log; exit 1; }
 echo "profiles done"
-for leg in ${ROW_LEGS:-c2 c3 c4 c5 afm h6}; do
+for leg in ${ROW_LEGS:-c2 c3 c4 c5 afm h6 h35}; do
   ROWS_ONLY=$leg timeout -k 10 400 python scripts/rowtable.py > $out/rows_$leg.json 2> $out/rows_$leg.err || { echo "rowtable $leg failed"; tail $out/rows_$leg.err; exit 1; }
   echo "rows $leg done"
 done

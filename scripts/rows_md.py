@@ -6,7 +6,8 @@ import sys
 ROWS = [("C2_M1_fm_rows", "M1 (C2)"), ("C3_H2_hhfm_catalog", "H2 (C3)"),
         ("C4_H2_hhfm_catalog_shard", "H2 (C4)"), ("C5_D1_dfm_bf16_mlp", "D1 (C5)"),
         ("C5_D1_dfm_fp32_mlp", "D1 (C5)"), ("A1_afm_rows", "A1"), ("A2_afm_catalog", "A2"),
-        ("H6_hhfm_train_step", "H6"), ("H6_afm_train_step", "H6"), ("H6_dfm_train_step", "H6")]
+        ("H6_hhfm_train_step", "H6"), ("H6_afm_train_step", "H6"), ("H6_dfm_train_step", "H6"),
+        ("H5_sample_negative", "H5")]
 
 
 def si(x):

@@ -69,6 +69,7 @@ def frappe_rows(rng, B, nu=957, ni=4082, ctx=(7, 2, 3)):
 
 
 res = {"host": platform.node(), "cpu_threads": THREADS}
+os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
 try:
     with open("/proc/cpuinfo") as f:
         res["cpu"] = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
@@ -249,6 +250,37 @@ if not only or "h6" in only:
         "unit": "steps/s", "gpu_ms_wall": ms, "gpu_rate": 1e3 / ms,
         "cpu_rate_numpy": 1.0 / c, "cpu_sample": "same batch, numpy oracle step"}
 
+
+# ---- H5 / H3: harness membership + walk on the device (Frappe-shape split) ------
+if not only or "h35" in only:
+    import tempfile
+    from hhfm_amd.NewLoadData import LoadData
+    from hhfm_amd.harness import Train
+
+    class _DevModel:
+        device = dev
+
+    with tempfile.TemporaryDirectory() as tmp:
+        np.random.seed(2016)
+        d = LoadData(bench.frappe_shape_dataset(tmp), "frappe_shape")
+    X = np.asarray(d.Train_data.values[:, 1:], dtype=np.int64)
+    host, devt = Train(data=d, model=None), Train(data=d, model=_DevModel())
+    np.random.seed(1)
+    devt.sample_negative(X, 50)               # builds the device pair arrays once
+    torch.cuda.synchronize()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        devt.sample_negative(X, 50)
+    t_dev = (time.perf_counter() - t0) / reps
+    t_host = cpu_s(lambda: host.sample_negative(X, 50), 3.0)
+    n = X.shape[0] * 50
+    res["H5_sample_negative"] = {
+        "config": f"sample_negative(Train rows, 50) on a Frappe-shape split ({X.shape[0]:,} rows; "
+                  "evaluate_AUC's draw), numpy RNG on the host, membership on the device",
+        "unit": "samples/s", "gpu_ms_wall": t_dev * 1e3, "gpu_rate": n / t_dev,
+        "cpu_rate_numpy": n / t_host,
+        "cpu_sample": "same call, host harness (vectorised membership, same stream)"}
 
 def _train_row(step, cpu_step, reps=20):
     step()
