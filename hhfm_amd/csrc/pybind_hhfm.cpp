@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "hhfm.h"
@@ -132,6 +133,31 @@ PYBIND11_MODULE(_hhfm, m) {
                                 P<void>(stream));
           }
           check(rc, "hhfm_topk_walk");
+        });
+
+  m.def("libfm_encode",
+        [](py::bytes buf, int ncols, int64_t max_rows, uptr labels, uptr ids, uptr distinct) {
+          std::string_view v = buf;
+          int64_t rows = 0, fm = 0;
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_libfm_encode(v.data(), (int64_t)v.size(), ncols, max_rows, P<double>(labels),
+                                   P<int64_t>(ids), &rows, &fm, P<int64_t>(distinct));
+          }
+          check(rc, "hhfm_libfm_encode");
+          return py::make_tuple(rows, fm);
+        });
+
+  m.def("loader_split",
+        [](uptr data, int64_t rows, int ncols, int item_col, int64_t test_size, uptr is_test) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_loader_split(P<const int64_t>(data), rows, ncols, item_col, test_size,
+                                   P<uint8_t>(is_test));
+          }
+          check(rc, "hhfm_loader_split");
         });
 
   m.def("topk_merge",

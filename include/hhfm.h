@@ -293,6 +293,29 @@ int hhfm_pf_contains(const int32_t* keys, int64_t nkeys, int32_t key_cols,
 int hhfm_topk_walk(const int32_t* pred, int64_t B, int32_t P, const int32_t* target,
                    const uint8_t* positive, int32_t TopK, int32_t* outcome, void* stream);
 
+/* ------------------------------------------------------------------------
+ * L1 — the libfm loader's per-cell work (NewLoadData.py:16-58), HOST code:
+ * every pointer below is host memory, nothing touches the GPU.
+ *
+ * hhfm_libfm_encode: parse `len` bytes of "label tok ... tok" lines
+ * (ncols fields separated by single spaces, blank lines skipped, at most
+ * max_rows rows) into labels [rows] (double) and ids [rows][ncols-1]
+ * (int64): the column-major first-occurrence token -> id map over columns
+ * 1.. (NewLoadData.py:29-34; identical tokens share an id across columns).
+ * distinct[ncols-1] = distinct tokens per column (n_user, n_item, ...:
+ * NewLoadData.py:22-23); *features_M = distinct tokens overall.
+ *
+ * hhfm_loader_split: over the shuffled rows data [rows][ncols] (label,
+ * user, item, ctx...), is_test[r] = 1 iff row r's key (every column but 0
+ * and item_col) is unseen and fewer than test_size rows went to Test so
+ * far (NewLoadData.py:46-58).
+ * ---------------------------------------------------------------------- */
+int hhfm_libfm_encode(const char* buf, int64_t len, int32_t ncols, int64_t max_rows,
+                      double* labels, int64_t* ids, int64_t* rows_out, int64_t* features_M,
+                      int64_t* distinct);
+int hhfm_loader_split(const int64_t* data, int64_t rows, int32_t ncols, int32_t item_col,
+                      int64_t test_size, uint8_t* is_test);
+
 #ifdef __cplusplus
 }
 #endif

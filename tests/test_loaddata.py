@@ -12,11 +12,14 @@ from hhfm_amd.NewLoadData import LoadData
 G = os.path.join(os.path.dirname(__file__), "golden")
 
 
+@pytest.mark.parametrize("encoder", ["native", "python"])
 @pytest.mark.parametrize("tag", ["frappe", "jiaju"])
-def test_loaddata_matches_reference(tag):
+def test_loaddata_matches_reference(tag, encoder):
+    """encoder="native": C++ tokenizer / id map / split walk (libhhfm.so host
+    code, hhfm_libfm_encode + hhfm_loader_split); "python": pandas."""
     ref = np.load(os.path.join(G, f"loaddata_{tag}.npz"))
     np.random.seed(2016)
-    d = LoadData(G + "/", f"synth_{tag}")
+    d = LoadData(G + "/", f"synth_{tag}", encoder=encoder)
     assert d.n_user == int(ref["n_user"]) and d.n_item == int(ref["n_item"])
     assert d.features_M == int(ref["features_M"])
     assert list(d.Train_data.columns) == list(ref["columns"])
@@ -49,13 +52,14 @@ def test_loaddata_shared_token_ids():
 REAL = "/root/reference/data/positive/"
 
 
+@pytest.mark.parametrize("encoder", ["native", "python"])
 @pytest.mark.skipif(not os.path.exists(REAL + "frappe/frappe.libfm"),
                     reason="real Frappe only exists in the builder container")
-def test_loaddata_real_frappe_hashes():
+def test_loaddata_real_frappe_hashes(encoder):
     with open(os.path.join(G, "frappe_real.json")) as f:
         ref = json.load(f)
     np.random.seed(2016)
-    d = LoadData(REAL, "frappe")
+    d = LoadData(REAL, "frappe", encoder=encoder)
     assert [d.n_user, d.n_item, d.features_M] == ref["sizes"]
     assert hashlib.sha256(np.ascontiguousarray(d.Train_data.values, np.int64)).hexdigest() == ref["train_sha256"]
     assert hashlib.sha256(np.ascontiguousarray(d.Test_data.values, np.int64)).hexdigest() == ref["test_sha256"]
@@ -83,3 +87,29 @@ def test_hr_at_k_real_frappe_matches_reference_harness():
         t.TopK = topk
         np.random.seed(31)
         assert t.evaluate_TopK(d.Test_data) == ref[f"hhfm_random_w_topk{topk}"]
+
+
+def test_loaddata_native_equals_python_frappe_shape(tmp_path):
+    """Frappe-shape synthetic libfm (96k rows of string tokens): the C++
+    encoder + split walk give the pandas path's fields exactly, and consume
+    the same numpy RNG draws."""
+    import bench
+    path = bench.frappe_shape_dataset(str(tmp_path))
+    out, nxt = {}, {}
+    for enc in ("native", "python"):
+        np.random.seed(2016)
+        out[enc] = LoadData(path, "frappe_shape", encoder=enc)
+        nxt[enc] = np.random.randint(1 << 30)
+    a, b = out["native"], out["python"]
+    assert (a.n_user, a.n_item, a.features_M) == (b.n_user, b.n_item, b.features_M)
+    assert np.array_equal(a.Train_data.values, b.Train_data.values)
+    assert np.array_equal(a.Test_data.values, b.Test_data.values)
+    assert a.positive_feedback == b.positive_feedback and a.train_set == b.train_set
+    assert nxt["native"] == nxt["python"]
+
+
+def test_libfm_encode_rejects_ragged_rows(tmp_path):
+    (tmp_path / "bad").mkdir()
+    (tmp_path / "bad" / "bad.libfm").write_text("1 a b c\n1 a b\n")
+    with pytest.raises(ValueError):
+        LoadData(str(tmp_path) + "/", "bad", encoder="native")
