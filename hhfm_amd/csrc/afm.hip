@@ -103,12 +103,19 @@ static void allow_lds(const void* fn, size_t bytes) {
   if (bytes > 65536)
     (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
-static size_t afm_rows_fused_lds(int k, int A) {
+static size_t afm_rows_fused_lds(int k, int A, bool split) {
   const int NA = (A + 31) / 32 * 32;
-  return 4 * (size_t)(NA * k + k + 2 * NA + 4 * 32 * 4);   // + 4 waves x 32 combos x float4
+  const size_t img = split ? (size_t)NA * k * 3 / 2 : (size_t)NA * k;   // 3 bf16 pieces or fp32
+  return 4 * (img + k + 2 * NA + 4 * 32 * 4);   // + 4 waves x 32 combos x float4
 }
 
-template <bool TBF, int NT>
+// SPLIT (k % 16 == 0): the attention GEMM on v_mfma_f32_32x32x16_bf16 with
+// both fp32 operands split into three bf16 pieces (split3x8): Wᵀ once into
+// three bf16 LDS images, the pair products in registers per 16 k; the six
+// piece products of order >= 2^-16, 6 MFMAs per 16 k instead of 8
+// 32x32x2_f32 ones (512 -> 192 cycles).  A 16-k step's lane half h holds k
+// {16t+4h .. +3} and {16t+8+4h .. +3}: two of the exact kernel's 8-k steps.
+template <bool TBF, int NT, bool SPLIT>
 __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_fused(
     const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
     int k, const float* __restrict__ w, float w0, const float* __restrict__ Wt,
@@ -117,7 +124,8 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
   constexpr int NA = NT * 32;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_rows_fused_lds()
   float4* img = reinterpret_cast<float4*>(smem);
-  float* Pl = smem + NA * k;
+  uint4* imgb = reinterpret_cast<uint4*>(smem);   // SPLIT: 3 piece images [NA][k/8] x 16 B
+  float* Pl = smem + (SPLIT ? NA * k * 3 / 2 : NA * k);
   float* bl = Pl + k;
   float* apl = bl + NA;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
@@ -126,11 +134,34 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
   int sw = 1;                                // XOR group: largest power of 2 dividing U, <= 16
   while (sw < 16 && U % (2 * sw) == 0) sw *= 2;
   const int SW = sw - 1;
-  for (int x = tid; x < NA * U; x += 256) {
-    const int u = x / U, c = x - u * U;
-    const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    img[u * U + (c ^ (u & SW))] = v;
+  const int U2 = k / 8;                      // SPLIT: 16-B bf16 units per Wᵀ row
+  int sw2 = 1;
+  while (sw2 < 16 && U2 % (2 * sw2) == 0) sw2 *= 2;
+  const int SW2 = sw2 - 1;
+  if constexpr (SPLIT) {
+    for (int x = tid; x < NA * U2; x += 256) {
+      const int u = x / U2, c = x - u * U2;
+      const int kb = 16 * (c >> 1) + 4 * (c & 1);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = u < A ? Wt[(int64_t)u * k + kb + e] : 0.f;
+        v[4 + e] = u < A ? Wt[(int64_t)u * k + kb + 8 + e] : 0.f;
+      }
+      bf16x8 q0, q1, q2;
+      split3x8(v, q0, q1, q2);
+      const int o = u * U2 + (c ^ (u & SW2));
+      imgb[o] = __builtin_bit_cast(uint4, q0);
+      imgb[NA * U2 + o] = __builtin_bit_cast(uint4, q1);
+      imgb[2 * NA * U2 + o] = __builtin_bit_cast(uint4, q2);
+    }
+  } else {
+    for (int x = tid; x < NA * U; x += 256) {
+      const int u = x / U, c = x - u * U;
+      const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      img[u * U + (c ^ (u & SW))] = v;
+    }
   }
   for (int x = tid; x < k; x += 256) Pl[x] = P[x];
   for (int x = tid; x < NA; x += 256) {
@@ -176,10 +207,11 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
   // chain never stalls a block start.
   int64_t blk = (int64_t)blockIdx.x * 4 + wv;
   int64_t ia = 0, ib = 0;
-  float4 xa = make_float4(0.f, 0.f, 0.f, 0.f), ya = xa;
+  float4 xa = make_float4(0.f, 0.f, 0.f, 0.f), ya = xa, xb = xa, yb = xa;
   if (blk < nblk) {
     ids_of(blk, ia, ib);
     gather(ia, ib, 0, xa, ya);
+    if constexpr (SPLIT) gather(ia, ib, 1, xb, yb);
   }
   for (; blk < nblk; blk += wstride) {
     const int64_t row = blk * R + r;
@@ -195,6 +227,48 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
     float sP = 0.f;
     // Σw of the row: lanes p < F of the row's group fetch one field each
     const float wf = (ok && p < F) ? w[clamp_id(idx[row * F + p], M)] : 0.f;
+    if constexpr (SPLIT) {
+      for (int t2 = 0; t2 < KQ / 2; ++t2) {
+        // steps 2t2, 2t2+1 are in (xa, ya), (xb, yb); fetch the next pair
+        float4 xn = xa, yn = ya, xm = xb, ym = yb;
+        if (2 * t2 + 2 < KQ) {
+          gather(ia, ib, 2 * t2 + 2, xn, yn);
+          gather(ia, ib, 2 * t2 + 3, xm, ym);
+        } else if (has_next) {
+          gather(na, nb, 0, xn, yn);
+          gather(na, nb, 1, xm, ym);
+        }
+        const int c0 = 16 * t2 + 4 * h;
+        const float ea[8] = {xa.x, xa.y, xa.z, xa.w, xb.x, xb.y, xb.z, xb.w};
+        const float eb[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
+        float pe[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pe[e] = ea[e] * eb[e];
+          sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
+        }
+        bf16x8 b0, b1, b2;
+        split3x8(pe, b0, b1, b2);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int u = 32 * n + j;          // A-operand row = attention unit
+          const int o = u * U2 + ((2 * t2 + h) ^ (u & SW2));
+          const bf16x8 a0 = __builtin_bit_cast(bf16x8, imgb[o]);
+          const bf16x8 a1 = __builtin_bit_cast(bf16x8, imgb[NA * U2 + o]);
+          const bf16x8 a2 = __builtin_bit_cast(bf16x8, imgb[2 * NA * U2 + o]);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[n], 0, 0, 0);
+        }
+        xa = xn;
+        ya = yn;
+        xb = xm;
+        yb = ym;
+      }
+    } else
     for (int t = 0; t < KQ; ++t) {
       float4 xn = xa, yn = ya;
       if (t + 1 < KQ) gather(ia, ib, t + 1, xn, yn);
@@ -593,17 +667,21 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       int64_t blocks = (nblk + 3) / 4;
       if (blocks > 2048) blocks = 2048;
       const bool tb = dtype == HHFM_BF16;
-      const size_t lds = afm_rows_fused_lds(k, A);
+      const char* ex = getenv("HHFM_AFM_EXACT");   // "1": the fp32-MFMA kernel (A/B)
+      const bool split = k % 16 == 0 && !(ex && ex[0] == '1');
+      const size_t lds = afm_rows_fused_lds(k, A, split);
+#define HHFM_AFM_FUSED_L(N, TB, SP)                                                         \
+  {                                                                                        \
+    allow_lds((const void*)afm_rows_fused<TB, N, SP>, lds);                                 \
+    hipLaunchKernelGGL((afm_rows_fused<TB, N, SP>), dim3((unsigned)blocks), dim3(256), lds, \
+                       st, idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out); \
+  }
 #define HHFM_AFM_FUSED(N)                                                                   \
   if (NT == N) {                                                                           \
     if (tb) {                                                                              \
-      allow_lds((const void*)afm_rows_fused<true, N>, lds);                                 \
-      hipLaunchKernelGGL((afm_rows_fused<true, N>), dim3((unsigned)blocks), dim3(256), lds, st, \
-                         idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
+      if (split) HHFM_AFM_FUSED_L(N, true, true) else HHFM_AFM_FUSED_L(N, true, false)     \
     } else {                                                                               \
-      allow_lds((const void*)afm_rows_fused<false, N>, lds);                                \
-      hipLaunchKernelGGL((afm_rows_fused<false, N>), dim3((unsigned)blocks), dim3(256), lds, st, \
-                         idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out);  \
+      if (split) HHFM_AFM_FUSED_L(N, false, true) else HHFM_AFM_FUSED_L(N, false, false)   \
     }                                                                                      \
     return (int)hipGetLastError();                                                         \
   }
@@ -612,6 +690,7 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       HHFM_AFM_FUSED(3)
       HHFM_AFM_FUSED(4)
 #undef HHFM_AFM_FUSED
+#undef HHFM_AFM_FUSED_L
     }
   }
   const int ntl = (A + GBN - 1) / GBN;

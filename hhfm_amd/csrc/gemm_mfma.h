@@ -15,6 +15,33 @@ namespace hhfm {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
+// fp32 -> three bf16 pieces, x == p0 + p1 + p2 exactly for normal x: p0 =
+// RNE(x) takes the top 8 significant bits, x - p0 is exact (Sterbenz) and
+// keeps <= 16, the next piece 8 of those, the last piece the rest.
+HHFM_DEV uint32_t bf16x2_rne(float lo, float hi) {   // v_cvt_pk_bf16_f32
+  typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+  const bf16x2v v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+HHFM_DEV void split3x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+  u32x4_t w0, w1, w2;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const float a = x[2 * v], b = x[2 * v + 1];
+    const uint32_t u0 = bf16x2_rne(a, b);
+    const float ra = a - __uint_as_float(u0 << 16), rb = b - __uint_as_float(u0 & 0xffff0000u);
+    const uint32_t u1 = bf16x2_rne(ra, rb);
+    const uint32_t u2 = bf16x2_rne(ra - __uint_as_float(u1 << 16),
+                                   rb - __uint_as_float(u1 & 0xffff0000u));
+    w0[v] = u0;
+    w1[v] = u1;
+    w2[v] = u2;
+  }
+  p0 = __builtin_bit_cast(bf16x8, w0);
+  p1 = __builtin_bit_cast(bf16x8, w1);
+  p2 = __builtin_bit_cast(bf16x8, w2);
+}
+
 constexpr int GBM = 128, GBN = 128;
 
 struct GemmArgs {

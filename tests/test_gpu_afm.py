@@ -1,6 +1,7 @@
 """AFM (K4) on the GPU vs the reference graph (golden afm.npz) and vs the
-oracle at Frappe shape.  fp32 throughout (exact-fp32 MFMA); tolerance 1e-5
-of the natural magnitude of each reduction."""
+oracle at Frappe shape.  fp32 numerics (exact-fp32 MFMA, or split-bf16 MFMA
+for the fused rows kernel when k % 16 == 0 — HHFM_AFM_EXACT=1 forces the
+former); tolerance 1e-5 of the natural magnitude of each reduction."""
 import os
 
 import numpy as np
@@ -40,8 +41,10 @@ def test_afm_vs_reference_graph():
     assert mism == 0, (mism, amb)
 
 
-@pytest.mark.parametrize("k,A", [(64, 64), (32, 16), (128, 128), (64, 32)])
-def test_afm_frappe_shape(k, A):
+@pytest.mark.parametrize("exact", ["0", "1"])
+@pytest.mark.parametrize("k,A", [(64, 64), (32, 16), (128, 128), (64, 32), (24, 32)])
+def test_afm_frappe_shape(k, A, exact, monkeypatch):
+    monkeypatch.setenv("HHFM_AFM_EXACT", exact)
     rng = np.random.default_rng(k + A)
     nu, ni = 957, 4082
     M = nu + ni + 12
