@@ -451,7 +451,10 @@ __global__ __launch_bounds__(256) void afm_cat_finish(
 // (AFM.py:232-243) is written once per (query, item) for hhfm_topk_dense.
 constexpr int kAfmCatFusedMaxUF = 7;
 
-template <bool TBF, int NT>
+// SPLIT (k % 16 == 0): as afm_rows_fused — Wᵀ as three bf16 LDS images, the
+// pair product uf_f ⊙ item split in registers per 16 k, 6 bf16 MFMAs per
+// 16 k instead of 8 fp32 ones.
+template <bool TBF, int NT, bool SPLIT>
 __global__ __launch_bounds__(256) void afm_cat_fused(
     const int32_t* __restrict__ q, int64_t nq, int F, const void* __restrict__ E, int64_t M,
     int k, const float* __restrict__ Wt, const float* __restrict__ att_b,
@@ -462,7 +465,8 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
   constexpr int NA = NT * 32;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_cat_fused_lds()
   float4* img = reinterpret_cast<float4*>(smem);
-  float* Pl = smem + NA * k;
+  uint4* imgb = reinterpret_cast<uint4*>(smem);   // SPLIT: 3 piece images [NA][k/8] x 16 B
+  float* Pl = smem + (SPLIT ? NA * k * 3 / 2 : NA * k);
   float* bl = Pl + kAfmMaxK;
   float* apl = bl + NA;
   float* ufl = apl + NA;                     // [4 waves][uF][k]
@@ -475,11 +479,34 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
   const int SW = sw - 1;
   const int64_t qg = blockIdx.x / nchunk;
   const int chunk = (int)(blockIdx.x - qg * nchunk);
-  for (int x = tid; x < NA * U; x += 256) {
-    const int u = x / U, c = x - u * U;
-    const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    img[u * U + (c ^ (u & SW))] = v;
+  const int U2 = k / 8;
+  int sw2 = 1;
+  while (sw2 < 16 && U2 % (2 * sw2) == 0) sw2 *= 2;
+  const int SW2 = sw2 - 1;
+  if constexpr (SPLIT) {
+    for (int x = tid; x < NA * U2; x += 256) {
+      const int u = x / U2, c = x - u * U2;
+      const int kb = 16 * (c >> 1) + 4 * (c & 1);
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = u < A ? Wt[(int64_t)u * k + kb + e] : 0.f;
+        v[4 + e] = u < A ? Wt[(int64_t)u * k + kb + 8 + e] : 0.f;
+      }
+      bf16x8 q0, q1, q2;
+      split3x8(v, q0, q1, q2);
+      const int o = u * U2 + (c ^ (u & SW2));
+      imgb[o] = __builtin_bit_cast(uint4, q0);
+      imgb[NA * U2 + o] = __builtin_bit_cast(uint4, q1);
+      imgb[2 * NA * U2 + o] = __builtin_bit_cast(uint4, q2);
+    }
+  } else {
+    for (int x = tid; x < NA * U; x += 256) {
+      const int u = x / U, c = x - u * U;
+      const float4 v = u < A ? *reinterpret_cast<const float4*>(Wt + (int64_t)u * k + 4 * c)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+      img[u * U + (c ^ (u & SW))] = v;
+    }
   }
   for (int x = tid; x < k; x += 256) Pl[x] = P[x];
   for (int x = tid; x < NA; x += 256) {
@@ -527,6 +554,73 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
       for (int x = 0; x < 16; ++x) acc[n][x] = 0.f;
     float sP = 0.f, num = 0.f, den = 0.f;
     float4 xa = gather(0);
+    // field f done: its logit from the accumulators, raw exp (AFM.py:230)
+    auto finish_field = [&]() {
+      float lg = 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int u = 32 * n + 8 * g4 + 4 * h;
+          const float4 bq = *reinterpret_cast<const float4*>(bl + u);
+          const float4 pq = *reinterpret_cast<const float4*>(apl + u);
+          const float bv[4] = {bq.x, bq.y, bq.z, bq.w}, pv[4] = {pq.x, pq.y, pq.z, pq.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            lg = fmaf(fmaxf(acc[n][4 * g4 + e] + bv[e], 0.f), pv[e], lg);
+            acc[n][4 * g4 + e] = 0.f;
+          }
+        }
+      lg += __shfl_xor(lg, 32, kWave);
+      sP += __shfl_xor(sP, 32, kWave);
+      const float a = expf(lg);
+      num = fmaf(a, sP, num);
+      den += a;
+      sP = 0.f;
+    };
+    if constexpr (SPLIT) {
+      float4 xb = gather(1);
+      const int K2 = KQ / 2;
+      for (int s = 0, f = 0, t2 = 0; s < uF * K2; ++s) {
+        // the item's steps 2t2, 2t2+1 are in xa, xb; fetch the next pair
+        // (the item row again from step 0 when the field wraps)
+        const bool last = s + 1 == uF * K2;
+        const int nt = t2 + 1 < K2 ? t2 + 1 : 0;
+        const float4 xn = last ? xa : gather(2 * nt), xm = last ? xb : gather(2 * nt + 1);
+        const int c0 = 16 * t2 + 4 * h;
+        const float4 ua = *reinterpret_cast<const float4*>(uq + f * k + c0);
+        const float4 ub = *reinterpret_cast<const float4*>(uq + f * k + c0 + 8);
+        float pe[8] = {xa.x * ua.x, xa.y * ua.y, xa.z * ua.z, xa.w * ua.w,
+                       xb.x * ub.x, xb.y * ub.y, xb.z * ub.z, xb.w * ub.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
+        bf16x8 b0, b1, b2;
+        split3x8(pe, b0, b1, b2);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int u = 32 * n + j;
+          const int o = u * U2 + ((2 * t2 + h) ^ (u & SW2));
+          const bf16x8 a0 = __builtin_bit_cast(bf16x8, imgb[o]);
+          const bf16x8 a1 = __builtin_bit_cast(bf16x8, imgb[NA * U2 + o]);
+          const bf16x8 a2 = __builtin_bit_cast(bf16x8, imgb[2 * NA * U2 + o]);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[n], 0, 0, 0);
+        }
+        xa = xn;
+        xb = xm;
+        if (++t2 == K2) {
+          finish_field();
+          t2 = 0;
+          ++f;
+        }
+      }
+      if (ok && h == 0) scores[b * N + item] = (ud + num) / (sa + den) + w[id];
+      continue;
+    }
     for (int s = 0, f = 0, t = 0; s < S; ++s) {
       const float4 xn = (s + 1 < S) ? gather(t + 1 < KQ ? t + 1 : 0) : xa;
       const int c0 = 8 * t + 4 * h;
@@ -544,28 +638,8 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
         acc[n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, pe[3], acc[n], 0, 0, 0);
       }
       xa = xn;
-      if (++t == KQ) {   // field f done: its logit, raw exp (AFM.py:230)
-        float lg = 0.f;
-#pragma unroll
-        for (int n = 0; n < NT; ++n)
-#pragma unroll
-          for (int g4 = 0; g4 < 4; ++g4) {
-            const int u = 32 * n + 8 * g4 + 4 * h;
-            const float4 bq = *reinterpret_cast<const float4*>(bl + u);
-            const float4 pq = *reinterpret_cast<const float4*>(apl + u);
-            const float bv[4] = {bq.x, bq.y, bq.z, bq.w}, pv[4] = {pq.x, pq.y, pq.z, pq.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              lg = fmaf(fmaxf(acc[n][4 * g4 + e] + bv[e], 0.f), pv[e], lg);
-              acc[n][4 * g4 + e] = 0.f;
-            }
-          }
-        lg += __shfl_xor(lg, 32, kWave);
-        sP += __shfl_xor(sP, 32, kWave);
-        const float a = expf(lg);
-        num = fmaf(a, sP, num);
-        den += a;
-        sP = 0.f;
+      if (++t == KQ) {   // field f done
+        finish_field();
         t = 0;
         ++f;
       }
@@ -574,9 +648,10 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
   }
 }
 
-static size_t afm_cat_fused_lds(int F, int k, int A) {
+static size_t afm_cat_fused_lds(int F, int k, int A, bool split) {
   const int NA = (A + 31) / 32 * 32;
-  return 4 * (size_t)(NA * k + kAfmMaxK + 2 * NA + 4 * (F - 1) * k);
+  const size_t img = split ? (size_t)NA * k * 3 / 2 : (size_t)NA * k;
+  return 4 * (img + kAfmMaxK + 2 * NA + 4 * (size_t)(F - 1) * k);
 }
 
 // fused A2 envelope: Wᵀ padded to NT*32 <= 128 rows, <= 7 query fields, the
@@ -588,7 +663,14 @@ static bool afm_cat_fused_ok(int F, int k, int A) {
   }();
   const int NT = (A + 31) / 32;
   return !gemm && F - 1 <= kAfmCatFusedMaxUF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 &&
-         afm_cat_fused_lds(F, k, A) <= 160 * 1024;
+         afm_cat_fused_lds(F, k, A, false) <= 160 * 1024;
+}
+
+// split-bf16 variant of the fused kernels: k % 16 == 0, its LDS images fit,
+// and HHFM_AFM_EXACT != 1
+static bool afm_split(int F, int k, int A) {
+  const char* e = getenv("HHFM_AFM_EXACT");
+  return k % 16 == 0 && !(e && e[0] == '1') && afm_cat_fused_lds(F, k, A, true) <= 160 * 1024;
 }
 
 struct AfmCatPlan {
@@ -668,7 +750,8 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       if (blocks > 2048) blocks = 2048;
       const bool tb = dtype == HHFM_BF16;
       const char* ex = getenv("HHFM_AFM_EXACT");   // "1": the fp32-MFMA kernel (A/B)
-      const bool split = k % 16 == 0 && !(ex && ex[0] == '1');
+      const bool split = k % 16 == 0 && !(ex && ex[0] == '1') &&
+                         afm_rows_fused_lds(k, A, true) <= 160 * 1024;
       const size_t lds = afm_rows_fused_lds(k, A, split);
 #define HHFM_AFM_FUSED_L(N, TB, SP)                                                         \
   {                                                                                        \
@@ -777,26 +860,30 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
       nchunk = (ntile + tpb - 1) / tpb;
       const dim3 grid((unsigned)(qgroups * nchunk));
       const int NT = (A + 31) / 32;
-      const size_t lds = afm_cat_fused_lds(F, k, A);
-#define HHFM_AFM_CAT_FUSED(N)                                                               \
-  if (NT == N) {                                                                           \
-    if (tb) {                                                                              \
-      allow_lds((const void*)afm_cat_fused<true, N>, lds);                                  \
-      hipLaunchKernelGGL((afm_cat_fused<true, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, F, \
-                         E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                   \
-                         (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
-    } else {                                                                               \
-      allow_lds((const void*)afm_cat_fused<false, N>, lds);                                 \
-      hipLaunchKernelGGL((afm_cat_fused<false, N>), grid, dim3(256), lds, st, qidx + b0 * F, nq, \
-                         F, E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                \
-                         (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);      \
-    }                                                                                      \
+      const bool split = afm_split(F, k, A);
+      const size_t lds = afm_cat_fused_lds(F, k, A, split);
+#define HHFM_AFM_CAT_FUSED_L(N, TB, SP)                                                       \
+  {                                                                                          \
+    allow_lds((const void*)afm_cat_fused<TB, N, SP>, lds);                                    \
+    hipLaunchKernelGGL((afm_cat_fused<TB, N, SP>), grid, dim3(256), lds, st, qidx + b0 * F,   \
+                       nq, F, E, features_M, k, Wt, att_b, att_p, A, P, ud, sa,                \
+                       (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);          \
+  }
+#define HHFM_AFM_CAT_FUSED(N)                                                                 \
+  if (NT == N) {                                                                             \
+    if (tb) {                                                                                \
+      if (split) HHFM_AFM_CAT_FUSED_L(N, true, true) else HHFM_AFM_CAT_FUSED_L(N, true, false) \
+    } else {                                                                                 \
+      if (split) HHFM_AFM_CAT_FUSED_L(N, false, true)                                        \
+      else HHFM_AFM_CAT_FUSED_L(N, false, false)                                             \
+    }                                                                                        \
   }
       HHFM_AFM_CAT_FUSED(1)
       HHFM_AFM_CAT_FUSED(2)
       HHFM_AFM_CAT_FUSED(3)
       HHFM_AFM_CAT_FUSED(4)
 #undef HHFM_AFM_CAT_FUSED
+#undef HHFM_AFM_CAT_FUSED_L
     } else {
       GemmArgs g{};
       g.M = item_count;
