@@ -47,10 +47,11 @@ def parse():
                    help="CPU-baseline time budget (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 21)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
-    p.add_argument("--legs", default="hr,catalog,catalog_bf16",
+    p.add_argument("--legs", default="hr,catalog,catalog_bf16,c3",
                    help="extra legs: hr (HR@10 identity after GPU training on Frappe-shape "
                         "data), catalog / catalog_bf16 (C4 item-sharded top-K over an fp32 / "
-                        "bf16 table, RCCL all-gather at N>1)")
+                        "bf16 table, RCCL all-gather at N>1), c3 (configs[2]: Frappe-catalog "
+                        "top-20, rank 0)")
     p.add_argument("--hr-epochs", type=int, default=5)
     return p.parse_args()
 
@@ -176,6 +177,41 @@ def hr_leg(dev, epochs):
             "model": f"HHFM k=64 trained {epochs} epochs on the GPU (partial_fit kernels), "
                      "evaluate_TopK TopK=10 (3000 rows)",
             "epoch_loss": losses, "train_s": t_train}
+
+
+def catalog_c3_leg(dev, reps=50):
+    """configs[2] / C3: HHFM k=64, bf16 table, Frappe vocabulary (957 users,
+    4,082 items, ctx 7/2/3), 3,000 queries, top-20 over the full catalog
+    (hhfm_catalog_topk: score matrix by MFMA GEMM + dense top-K)."""
+    from hhfm_amd import ops
+    nu, ni, ctx, k, B = 957, 4082, (7, 2, 3), 64, 3000
+    g = torch.Generator(device=dev)
+    g.manual_seed(2)
+    M = nu + ni + sum(ctx)
+    E = (torch.randn(M, k, generator=g, device=dev) * 0.01).to(torch.bfloat16)
+    cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
+            torch.randint(nu, nu + ni, (B,), generator=g, device=dev)]
+    off = nu + ni
+    for c in ctx:
+        cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+        off += c
+    A = torch.stack(cols, 1).to(torch.int32).contiguous()
+
+    def step():
+        return ops.catalog_topk(A, E, ops.MODE_HHFM, 20, nu, ni, 0, None, 0, (2, 5), (0, 0))
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / reps * 1e3
+    pairs = B * ni
+    return {"workload": "C3 (configs[2]): HHFM k=64 bf16 table, Frappe vocabulary, 3,000 "
+                        "queries x 4,082 items, top-20, one GPU", "ms_per_query_batch": ms,
+            "pairs_per_s": pairs / (ms * 1e-3), "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12}
 
 
 def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
@@ -324,6 +360,11 @@ def main():
         except Exception as e:  # noqa: BLE001
             extra["catalog_c4"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
+    if "c3" in legs and rank == 0:
+        try:
+            extra["catalog_c3"] = catalog_c3_leg(dev)
+        except Exception as e:  # noqa: BLE001
+            extra["catalog_c3"] = {"error": f"{type(e).__name__}: {e}"}
     if "catalog_bf16" in legs:
         try:
             extra["catalog_c4_bf16"] = catalog_leg(dev, world, rank, table_dtype=torch.bfloat16)
