@@ -130,7 +130,11 @@ HHFM_DEV void insert_one(float* ls, int32_t* li, float s, int32_t it, int K) {
 // order >= 2^-16 (the dropped ones are < 2^-24 relative), 6 MFMAs per 16 k
 // instead of 8.  The result differs from the k-ordered fmaf chain only in
 // fp32 accumulation order (~1e-7 relative; tolerance 1e-5, north_star).
-template <bool BF16, int KT, int KPAD, bool FM, bool SPLIT>
+// STORE: no selection — the score tile is written to the score matrix
+// out_s [B][ostride_b] (the small-catalog path's scores for topk_dense).  The
+// MFMA operands are swapped (queries as A, items as B) so a lane's column is
+// an item: each store instruction writes 32 consecutive items of a query row.
+template <bool BF16, int KT, int KPAD, bool FM, bool SPLIT, bool STORE = false>
 __global__ __launch_bounds__(256) void catalog_main(
     const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
     const char* __restrict__ E, int64_t item_row_begin, int32_t N,
@@ -224,6 +228,11 @@ __global__ __launch_bounds__(256) void catalog_main(
     if constexpr (PF == 2) load_tile(tb0 + 1, a1, wi1);
   }
 
+  // A x B on the bf16 MFMA; STORE swaps the roles (queries as A)
+  auto mma16 = [&](const bf16x8& x, const bf16x8& y, const f32x16& c) {
+    return STORE ? __builtin_amdgcn_mfma_f32_32x32x16_bf16(y, x, c, 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+  };
   auto tile_step = [&](const int tile, uint4 (&ar)[KT], float& wr) {
     // global threshold hint: load now, consume after the MFMA chain
     const int32_t gk = (q < B) ? gthr[q] : 0;
@@ -240,9 +249,9 @@ __global__ __launch_bounds__(256) void catalog_main(
       for (int t = 0; t < KT; ++t) {
         const bf16x8 ai = __builtin_bit_cast(bf16x8, ar[t]);
         refill(t);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[2][t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[1][t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[0][t], acc, 0, 0, 0);
+        acc = mma16(ai, qp[2][t], acc);
+        acc = mma16(ai, qp[1][t], acc);
+        acc = mma16(ai, qp[0][t], acc);
       }
     } else if constexpr (SPLIT) {
 #pragma unroll
@@ -256,12 +265,12 @@ __global__ __launch_bounds__(256) void catalog_main(
         bf16x8 i0, i1, i2;
         split3x8(x, i0, i1, i2);
         // smallest terms first
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, qp[0][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[1][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[2][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[0][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[1][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[0][u], acc, 0, 0, 0);
+        acc = mma16(i2, qp[0][u], acc);
+        acc = mma16(i1, qp[1][u], acc);
+        acc = mma16(i0, qp[2][u], acc);
+        acc = mma16(i1, qp[0][u], acc);
+        acc = mma16(i0, qp[1][u], acc);
+        acc = mma16(i0, qp[0][u], acc);
       }
     } else
 #pragma unroll
@@ -287,17 +296,33 @@ __global__ __launch_bounds__(256) void catalog_main(
       }
 #pragma unroll
       for (int e = 0; e < EPC; ++e)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
+        acc = STORE ? __builtin_amdgcn_mfma_f32_32x32x2f32(bq[t][e], av[e], acc, 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
     }
     if constexpr (FM) {
       // D[i][j] += w_i * 1 + 1 * (q_j·f_j)   (bias row/col folded into one MFMA)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f,
-                                                 h == 0 ? 1.f : cq, acc, 0, 0, 0);
+      if constexpr (STORE)   // D[q][i] += (q_q·f_q) * 1 + 1 * w_i
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? cq : 1.f,
+                                                   h == 0 ? 1.f : wcur, acc, 0, 0, 0);
+      else
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f,
+                                                   h == 0 ? 1.f : cq, acc, 0, 0, 0);
       int item = nxt * kTile + j;
       item = item < N ? item : N - 1;
       wr = w ? w[item_row_begin + item] : 0.f;
     }
 
+    if constexpr (STORE) {   // rows = queries q0 + ..., column = item tile*32 + j
+      const int32_t item = tile * kTile + j;
+      if (item < item_end) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int64_t qr = q0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (qr < B) out_s[qr * ostride_b + item] = acc[r];
+        }
+      }
+      return;
+    }
     // ---- filter against the per-query K-th score ----
     // The threshold is the better of this split's K-th score and the best
     // K-th score any split has published for the query (gthr: monotone
@@ -388,6 +413,7 @@ __global__ __launch_bounds__(256) void catalog_main(
     for (int tile = tb0; tile < tb1; ++tile) tile_step(tile, a0, wi0);
   }
 
+  if constexpr (STORE) return;
   // ---- emit this split's sorted list per query ----
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
@@ -625,6 +651,13 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   return p;
 }
 
+// HHFM_CATALOG_DENSE_GEMM=1: the small-catalog score matrix from the shared
+// LDS-tiled fp32 GEMM instead of the catalog kernel's STORE variant (A/B)
+static bool catalog_dense_gemm() {
+  const char* e = getenv("HHFM_CATALOG_DENSE_GEMM");
+  return e && e[0] == '1';
+}
+
 // HHFM_CATALOG_EXACT=1 selects the fp32-MFMA (k-ordered fmaf chain) kernel
 // instead of the split-bf16 one (A/B and numerics comparisons).
 static bool catalog_exact() {
@@ -660,6 +693,43 @@ static bool dispatch_kt(int KT, const Plan& p, const float* H, const float* cst,
     case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
     case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
     case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    default: return false;
+  }
+  return true;
+}
+
+// small-catalog score matrix on the catalog kernel (STORE): any number of
+// item tiles per split (no top-K lists to warm up), ~2,048 workgroups
+template <bool BF16, int KT, bool FM>
+static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const float* cst,
+                         const char* E, int64_t irb, const float* w, float* sc, int64_t ldsc,
+                         int32_t* gthr, hipStream_t st) {
+  const int ntiles = (N + kTile - 1) / kTile;
+  int S = (2048 + nqb - 1) / nqb;
+  S = S > ntiles ? ntiles : (S < 1 ? 1 : S);
+  const int tps = (ntiles + S - 1) / S;
+  S = (ntiles + tps - 1) / tps;
+  constexpr bool kCanSplit = BF16 || KT >= 2;
+  if (kCanSplit && !catalog_exact())
+    hipLaunchKernelGGL((catalog_main<BF16, KT, 32, FM, kCanSplit, true>), dim3(nqb * S),
+                       dim3(256), 0, st, H, cst, B, E, irb, N, w, 1, S, tps, nqb, sc, nullptr,
+                       ldsc, 0, 0, gthr);
+  else
+    hipLaunchKernelGGL((catalog_main<BF16, KT, 32, FM, false, true>), dim3(nqb * S),
+                       dim3(256), 0, st, H, cst, B, E, irb, N, w, 1, S, tps, nqb, sc, nullptr,
+                       ldsc, 0, 0, gthr);
+}
+
+template <bool BF16, bool FM>
+static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H,
+                           const float* cst, const char* E, int64_t irb, const float* w,
+                           float* sc, int64_t ldsc, int32_t* gthr, hipStream_t st) {
+  switch (KT) {
+    case 1: launch_store<BF16, 1, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
+    case 2: launch_store<BF16, 2, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
+    case 4: launch_store<BF16, 4, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
+    case 8: launch_store<BF16, 8, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
+    case 16: launch_store<BF16, 16, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
     default: return false;
   }
   return true;
@@ -776,6 +846,19 @@ extern "C" int hhfm_catalog_topk(
 
   if (p.dense) {
     float* sc = reinterpret_cast<float*>(ws + p.off_sc);
+    if (!catalog_dense_gemm()) {   // the score matrix from the catalog kernel (STORE)
+      const bool fmm = mode == HHFM_MODE_FM;
+      const float* wv = (fmm && w) ? w : nullptr;
+      bool ok;
+      if (bf16) ok = fmm ? dispatch_store<true, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st)
+                         : dispatch_store<true, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st);
+      else ok = fmm ? dispatch_store<false, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st)
+                    : dispatch_store<false, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st);
+      if (ok) {
+        launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st);
+        return (int)hipGetLastError();
+      }
+    }
     GemmArgs g{};
     g.M = B;
     g.N = item_count;

@@ -153,15 +153,16 @@ def test_catalog_topk_hhfm_parity(dtype, k, K):
     _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, _hhfm_scale(A, E, n_user, n_item))
 
 
-@pytest.mark.parametrize("exact", ["0", "1"])
+@pytest.mark.parametrize("variant", ["split", "exact", "gemm"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("k", [16, 64])
-def test_catalog_topk_fm_parity(dtype, k, exact, monkeypatch):
-    """Dense (score-matrix) path; HHFM_CATALOG_EXACT does not change it (its
-    fp32 MFMA GEMM is not the bottleneck: a split-bf16 GEMM over K = 3k
-    measured the same C3 time)."""
+def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
+    """Dense (score-matrix) path: the catalog kernel's STORE variant on
+    split-bf16 MFMA (default) or fp32 MFMA (HHFM_CATALOG_EXACT=1), or the
+    shared fp32 GEMM (HHFM_CATALOG_DENSE_GEMM=1), then the dense top-K."""
     from hhfm_amd import ops
-    monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
+    monkeypatch.setenv("HHFM_CATALOG_EXACT", "1" if variant == "exact" else "0")
+    monkeypatch.setenv("HHFM_CATALOG_DENSE_GEMM", "1" if variant == "gemm" else "0")
     rng = np.random.default_rng(5 + k)
     n_user, n_item = 957, 4082
     A, M = synth_rows(rng, 257, n_user, n_item, (7, 2, 3))
