@@ -188,8 +188,8 @@ def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
 def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
     """Catalogs above the small-catalog bound (N > 16384) take the streaming
     threshold kernel (split-bf16 MFMA by default, the fp32-MFMA fmaf chain
-    with HHFM_CATALOG_EXACT=1); the 4082-item cases above take the dense
-    score matrix."""
+    with HHFM_CATALOG_EXACT=1); the
+    4082-item cases above take the dense score matrix."""
     from hhfm_amd import ops
     monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
     rng = np.random.default_rng(17 + k + K)
