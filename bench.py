@@ -343,6 +343,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "fm_rows_fast<5,16,f32,w>", "kernel_ms": kern_ms,
+                     "traffic_GBps": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
+                     "traffic_frac": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                                     if traffic else None,
                      "algorithmic_bytes_per_row": bpr,
                      "survey_bytes_per_row": bpr_survey,
                      "survey_rate_GBps": bpr_survey * args.rows / (kern_ms * 1e-3) / 1e9},
