@@ -100,6 +100,11 @@ int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B, int32_t ncols,
  *   output:  top_score/top_idx [B][K], sorted by (score desc, index asc) —
  *            tf.nn.top_k order; top_idx = global_item_base + offset in range.
  *   K must be in [1, 64] and <= item_count.
+ *   arithmetic: the h·item products run on bf16 MFMA with every fp32
+ *            operand split exactly into three bf16 pieces (products of
+ *            order >= 2^-16 kept, fp32 accumulation: ~1e-7 relative to a
+ *            k-ordered fp32 chain); HHFM_CATALOG_EXACT=1 in the environment
+ *            selects the fp32-MFMA kernels (the k-ordered fmaf chain).
  * Workspace: query `hhfm_catalog_topk_workspace` with the same sizes.
  * ---------------------------------------------------------------------- */
 int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count, int32_t k,
