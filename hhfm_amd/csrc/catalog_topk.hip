@@ -30,6 +30,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_KO
 #define HHFM_MAIN_KO 0
 #endif
+#ifndef HHFM_STORE_WG
+#define HHFM_STORE_WG 2048   // STORE launch size (C3: 512-2048 equal, 4096 +15 %)
+#endif
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
 #endif
@@ -705,7 +708,7 @@ static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const fl
                          const char* E, int64_t irb, const float* w, float* sc, int64_t ldsc,
                          int32_t* gthr, hipStream_t st) {
   const int ntiles = (N + kTile - 1) / kTile;
-  int S = (2048 + nqb - 1) / nqb;
+  int S = (HHFM_STORE_WG + nqb - 1) / nqb;
   S = S > ntiles ? ntiles : (S < 1 ? 1 : S);
   const int tps = (ntiles + S - 1) / S;
   S = (ntiles + tps - 1) / tps;
