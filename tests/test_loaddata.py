@@ -113,3 +113,27 @@ def test_libfm_encode_rejects_ragged_rows(tmp_path):
     (tmp_path / "bad" / "bad.libfm").write_text("1 a b c\n1 a b\n")
     with pytest.raises(ValueError):
         LoadData(str(tmp_path) + "/", "bad", encoder="native")
+
+
+def test_libfm_encode_crlf_and_blank_lines(tmp_path):
+    """Windows line ends and blank lines: the C++ tokenizer gives the pandas
+    path's ids, labels and split (read_csv skips blank lines)."""
+    d = tmp_path / "crlf"
+    d.mkdir()
+    rng = np.random.default_rng(3)
+    lines = []
+    for r in range(400):
+        lines.append(f"{rng.choice([1, -1])} u{rng.integers(0, 30)} i{rng.integers(0, 50)} "
+                     f"c{rng.integers(0, 4)} d{rng.integers(0, 3)}")
+        if r % 97 == 0:
+            lines.append("")
+    (d / "crlf.libfm").write_bytes(("\r\n".join(lines) + "\r\n\r\n").encode())
+    out = {}
+    for enc in ("native", "python"):
+        np.random.seed(5)
+        out[enc] = LoadData(str(tmp_path) + "/", "crlf", encoder=enc)
+    a, b = out["native"], out["python"]
+    assert (a.n_user, a.n_item, a.features_M) == (b.n_user, b.n_item, b.features_M)
+    assert np.array_equal(a.Train_data.values, b.Train_data.values)
+    assert np.array_equal(a.Test_data.values, b.Test_data.values)
+    assert a.positive_feedback == b.positive_feedback
