@@ -341,21 +341,32 @@ __global__ __launch_bounds__(256) void catalog_main(
       return;
     }
 #endif
-    bool pass[16];
+    // survivors as wave ballots (SGPRs; a lane reads its own bit back where
+    // needed), and the item_end mask only on the split's partial last tile
+    uint64_t pm[16];
+    if (ibase + kTile <= item_end) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pm[r] = __ballot(acc[r] >= thr);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        pm[r] = __ballot(acc[r] >= thr && ibase + row < item_end);
+      }
+    }
     int count = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-      pass[r] = acc[r] >= thr && ibase + row < item_end;
-      count += __popcll(__ballot(pass[r]));
-    }
+    for (int r = 0; r < 16; ++r) count += __popcll(pm[r]);
     if (count == 0) return;
+    const uint64_t lbit = 1ull << l;
+#define HHFM_PASS(r) ((pm[r] & lbit) != 0)
+#define HHFM_PASSMASK(r) (pm[r])
 
     if (count <= kBulkMin) {
       // sparse: one wave-wide sorted insertion per surviving score
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        uint64_t m = __ballot(pass[r]);
+        uint64_t m = HHFM_PASSMASK(r);
         while (m) {
           const int L = __builtin_ctzll(m);
           m &= m - 1;
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(256) void catalog_main(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        T[j * kTile + (row ^ j)] = pass[r] ? acc[r] : kNegInf;
+        T[j * kTile + (row ^ j)] = HHFM_PASS(r) ? acc[r] : kNegInf;
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): tile visible to the wave
       __builtin_amdgcn_wave_barrier();
@@ -416,6 +427,8 @@ __global__ __launch_bounds__(256) void catalog_main(
     for (int tile = tb0; tile < tb1; ++tile) tile_step(tile, a0, wi0);
   }
 
+#undef HHFM_PASS
+#undef HHFM_PASSMASK
   if constexpr (STORE) return;
   // ---- emit this split's sorted list per query ----
   __builtin_amdgcn_s_waitcnt(0xc07f);
