@@ -30,6 +30,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_KO
 #define HHFM_MAIN_KO 0
 #endif
+#ifndef HHFM_MAIN_PRIO
+#define HHFM_MAIN_PRIO 1   // s_setprio(1) around the MFMA chain (C4 bf16 1.66 -> 1.48 ms)
+#endif
 #ifndef HHFM_STORE_WG
 #define HHFM_STORE_WG 2048   // STORE launch size (C3: 512-2048 equal, 4096 +15 %)
 #endif
@@ -247,6 +250,7 @@ __global__ __launch_bounds__(256) void catalog_main(
       item = item < N ? item : N - 1;
       ar[t] = *reinterpret_cast<const uint4*>(E + (item_row_begin + item) * ROWB + 16 * h + 32 * t);
     };
+    if (HHFM_MAIN_PRIO) __builtin_amdgcn_s_setprio(1);
     if constexpr (SPLIT && BF16) {
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
@@ -302,6 +306,7 @@ __global__ __launch_bounds__(256) void catalog_main(
         acc = STORE ? __builtin_amdgcn_mfma_f32_32x32x2f32(bq[t][e], av[e], acc, 0, 0, 0)
                     : __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
     }
+    if (HHFM_MAIN_PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (FM) {
       // D[i][j] += w_i * 1 + 1 * (q_j·f_j)   (bias row/col folded into one MFMA)
       if constexpr (STORE)   // D[q][i] += (q_q·f_q) * 1 + 1 * w_i
