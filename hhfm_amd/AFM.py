@@ -102,11 +102,15 @@ class AFM(ScoringModel):
                               float(self.weights["bias"]), Wt, b, p, P)
         return self._np_out(out)
 
-    def topk(self, A, tp):
-        q = self._idx(A)
+    def catalog_topk(self, q, begin, count, K):
+        """Top-K of items [begin, begin+count) by the attention score of
+        AFM.py:209-246 -> (scores, global item offsets) device tensors [B, K]."""
         Wt, b, p, P = self._att()
-        _, ids = ops.afm_catalog_topk(q, self.table, self.weights["feature_bias"].reshape(-1),
-                                      Wt, b, p, P, self.n_user, self.n_item, int(tp))
+        return ops.afm_catalog_topk(q, self.table, self.weights["feature_bias"].reshape(-1),
+                                    Wt, b, p, P, self.n_user + begin, count, int(K), begin)
+
+    def topk(self, A, tp):
+        _, ids = self.catalog_topk(self._idx(A), 0, self.n_item, tp)
         return ids.cpu().numpy()
 
     def _run_fetch(self, fetch, feed):

@@ -128,11 +128,16 @@ class DeepFM(ScoringModel):
                               dims, self.mlp_dtype, Wp, bp)
         return self._np_out(out)
 
-    def topk(self, A, tp):
-        q = self._idx(A)
+    def catalog_topk(self, q, begin, count, K):
+        """Top-K of items [begin, begin+count) by the DeepFM score of
+        DFM.py:219-231 -> (scores, global item offsets) device tensors [B, K]."""
         Wt, bs, dims, Wp, bp = self._prepared()
-        _, ids = ops.dfm_catalog_topk(q, self.table, self.weights["feature_bias"].reshape(-1),
-                                      Wt, bs, dims, Wp, bp, 1, self.n_user, self.n_item, int(tp))
+        return ops.dfm_catalog_topk(q, self.table, self.weights["feature_bias"].reshape(-1),
+                                    Wt, bs, dims, Wp, bp, 1, self.n_user + begin, count, int(K),
+                                    begin)
+
+    def topk(self, A, tp):
+        _, ids = self.catalog_topk(self._idx(A), 0, self.n_item, tp)
         return ids.cpu().numpy()
 
     def _run_fetch(self, fetch, feed):

@@ -89,13 +89,17 @@ class FM(ScoringModel):
         out = ops.fm_score_rows(idx, self.table, w, float(self.weights["bias"]))
         return self._np_out(out)
 
+    def catalog_topk(self, q, begin, count, K):
+        """Top-K of items [begin, begin+count) by (u+f)·(i+f) + w_i (FM.py:172-185)
+        -> (scores, global item offsets) device tensors [B, K]."""
+        ncols = q.shape[1]
+        return ops.catalog_topk(q, self.table, ops.MODE_FM, int(K), self.n_user + begin, count,
+                                begin, self.weights["feature_bias"].reshape(-1), 0,
+                                (2, ncols) if ncols > 2 else (0, 0), (0, 0))
+
     def topk(self, A, tp):
         """Top-``tp`` item offsets in [0, n_item) by (u+f)·(i+f) + w_i."""
-        q = self._idx(A)
-        ncols = q.shape[1]
-        _, ids = ops.catalog_topk(q, self.table, ops.MODE_FM, int(tp), self.n_user, self.n_item,
-                                  0, self.weights["feature_bias"].reshape(-1), 0,
-                                  (2, ncols) if ncols > 2 else (0, 0), (0, 0))
+        _, ids = self.catalog_topk(self._idx(A), 0, self.n_item, tp)
         return ids.cpu().numpy()
 
     def _run_fetch(self, fetch, feed):

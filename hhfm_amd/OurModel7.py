@@ -99,11 +99,15 @@ class OUR(ScoringModel):
         out = ops.hybrid_score_rows(idx, self.table, 0, 1, ctx, tim)
         return self._np_out(out)
 
-    def topk(self, A, tp):
-        q = self._idx(A)
+    def catalog_topk(self, q, begin, count, K):
+        """Top-K of items [begin, begin+count) by h·item (OurModel7.py:229-295)
+        -> (scores, global item offsets) device tensors [B, K]."""
         ctx, tim = self._ranges(q.shape[1])
-        _, ids = ops.catalog_topk(q, self.table, ops.MODE_HHFM, int(tp), self.n_user,
-                                  self.n_item, 0, None, 0, ctx, tim)
+        return ops.catalog_topk(q, self.table, ops.MODE_HHFM, int(K), self.n_user + begin,
+                                count, begin, None, 0, ctx, tim)
+
+    def topk(self, A, tp):
+        _, ids = self.catalog_topk(self._idx(A), 0, self.n_item, tp)
         return ids.cpu().numpy()
 
     def _run_fetch(self, fetch, feed):

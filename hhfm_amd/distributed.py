@@ -7,8 +7,8 @@ The reference ranks the whole catalog on one device with one tf.nn.top_k
      the rank's range);
   2. it computes its local top-K with hhfm_catalog_topk (scores fp32, ids
      already global item offsets);
-  3. one all-gather of (score, id) [B, K] per rank — RCCL over xGMI when the
-     process group is ``nccl``, gloo on CPU;
+  3. one all-gather of the packed (score bits, id) int32 [B, K, 2] per rank —
+     RCCL over xGMI when the process group is ``nccl``, gloo on CPU;
   4. hhfm_topk_merge (device) / hhfm_topk_merge_host merges the R sorted
      lists with the same (score desc, id asc) order, which reproduces the
      single-device ranking because ranges are contiguous and ordered.
@@ -47,18 +47,20 @@ def _pad(scores: torch.Tensor, ids: torch.Tensor, K: int):
 
 
 def gather_topk(scores: torch.Tensor, ids: torch.Tensor, group=None):
-    """All-gather each rank's [B,K] lists -> [R,B,K] (rank-major)."""
+    """All-gather each rank's [B,K] lists -> [R,B,K] (rank-major).
+
+    One collective: (score bits, id) are packed as an int32 [B,K,2] payload
+    (8 B per entry), so the latency-bound exchange is a single RCCL
+    all-gather instead of one per field."""
     world = dist.get_world_size(group)
     B, K = scores.shape
-    out_s = torch.empty(world, B, K, dtype=scores.dtype, device=scores.device)
-    out_i = torch.empty(world, B, K, dtype=ids.dtype, device=ids.device)
+    packed = torch.stack([scores.contiguous().view(torch.int32), ids.contiguous()], dim=2)
+    out = torch.empty(world, B, K, 2, dtype=torch.int32, device=packed.device)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out_s, scores.contiguous(), group=group)
-        dist.all_gather_into_tensor(out_i, ids.contiguous(), group=group)
+        dist.all_gather_into_tensor(out, packed, group=group)
     else:
-        dist.all_gather(list(out_s.unbind(0)), scores.contiguous(), group=group)
-        dist.all_gather(list(out_i.unbind(0)), ids.contiguous(), group=group)
-    return out_s, out_i
+        dist.all_gather(list(out.unbind(0)), packed, group=group)
+    return out[..., 0].contiguous().view(torch.float32), out[..., 1].contiguous()
 
 
 LocalScorer = Callable[[object, int, int, int], Tuple[torch.Tensor, torch.Tensor]]
@@ -93,18 +95,20 @@ def sharded_topk(A, K: int, n_item: int, local_scorer: LocalScorer, group=None):
 
 
 def model_scorer(model) -> LocalScorer:
-    """The HIP local scorer of an FM / OUR model for its rank's item range."""
+    """The HIP local scorer of a model for its rank's item range: each model
+    class scores items [begin, begin+count) with its own catalog kernel
+    (FM.py:172-185, OurModel7.py:229-295, AFM.py:209-246, DFM.py:219-231) and
+    reports global item offsets."""
+    from .AFM import AFM
+    from .DFM import DeepFM
+    from .FM import FM
+    from .OurModel7 import OUR
+    if not isinstance(model, (FM, OUR, AFM, DeepFM)):
+        raise TypeError(f"no sharded catalog scorer for {type(model).__name__}; "
+                        "expected FM, OUR, AFM or DeepFM")
+
     def score(A, begin, count, K):
-        q = model._idx(A)
-        ncols = q.shape[1]
-        if hasattr(model, "_ranges"):      # OUR (HHFM) model
-            ctx, tim = model._ranges(ncols)
-            mode, w = ops.MODE_HHFM, None
-        else:
-            ctx, tim = ((2, ncols) if ncols > 2 else (0, 0)), (0, 0)
-            mode, w = ops.MODE_FM, model.weights["feature_bias"].reshape(-1)
-        return ops.catalog_topk(q, model.table, mode, K, model.n_user + begin, count, begin,
-                                w, 0, ctx, tim)
+        return model.catalog_topk(model._idx(A), begin, count, K)
     return score
 
 

@@ -22,34 +22,53 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import cpu as ocpu
+    from oracle import fm_oracle as orc
     from tests.helpers import synth_rows, table
     rng = np.random.default_rng(42)
-    nu, ni = 300, 5000
+    nu, ni = 300, 5000 if mode != "afm" else 1200
     A, M = synth_rows(rng, 64, nu, ni, (7, 2, 3))
     E = table(rng, M, 32)
-    E[nu + 100] = E[nu + 4000]                  # a cross-shard exact tie
+    E[nu + 100] = E[nu + 1100]                  # a cross-shard exact tie
+    w = rng.normal(0, 0.01, M).astype(np.float32)
+    if mode == "afm":                           # AFM.py:209-246 (numpy oracle)
+        W = rng.normal(0, 0.2, (32, 16)).astype(np.float32)
+        b = rng.normal(0, 0.2, (1, 16)).astype(np.float32)
+        pv = rng.normal(0, 1, 16).astype(np.float32)
+        P = np.ones((32, 1), np.float32)
+        full = orc.afm_catalog_scores(A, E, w, W, b, pv, P, nu, ni)
 
     def scorer(A_, begin, count, K):
-        s, i = ocpu.catalog_topk(A_, E, 1, K, nu + begin, count, ctx=(2, 5), threads=1)
+        if mode == "afm":
+            s, i = orc.top_k(full[:, begin:begin + count], K)
+            return torch.from_numpy(np.ascontiguousarray(s)), \
+                torch.from_numpy((i + begin).astype(np.int32))
+        s, i = ocpu.catalog_topk(A_, E, 0 if mode == "fm" else 1, K, nu + begin, count,
+                                 w=w if mode == "fm" else None, ctx=(2, 5), threads=1)
         return torch.from_numpy(s), torch.from_numpy(i + begin)
 
     s, i = hd.sharded_topk(A, 20, ni, scorer)
     if rank == 0:
-        rs, ri = ocpu.catalog_topk(A, E, 1, 20, nu, ni, ctx=(2, 5), threads=1)
+        if mode == "afm":
+            rs, ri = orc.top_k(full, 20)
+        else:
+            rs, ri = ocpu.catalog_topk(A, E, 0 if mode == "fm" else 1, 20, nu, ni,
+                                       w=w if mode == "fm" else None, ctx=(2, 5), threads=1)
         q.put((np.array_equal(i.numpy(), ri), float(np.abs(s.numpy() - rs).max())))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_topk_gloo(world):
+@pytest.mark.parametrize("world,mode", [(2, "hhfm"), (3, "hhfm"), (2, "fm"), (2, "afm")])
+def test_sharded_topk_gloo(world, mode):
+    """Item-sharded top-K (shard split, one packed all-gather, host merge) ==
+    the single-device ranking, HHFM / FM / AFM score modes."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -57,6 +76,11 @@ def test_sharded_topk_gloo(world):
         assert p.exitcode == 0
     same, err = q.get(timeout=10)
     assert same and err == 0.0
+
+
+def test_model_scorer_rejects_unknown_models():
+    with pytest.raises(TypeError):
+        hd.model_scorer(object())
 
 
 def test_shard_range_partition():

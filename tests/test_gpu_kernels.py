@@ -11,10 +11,16 @@ import pytest
 import torch
 
 from oracle import fm_oracle as orc
-from tests.helpers import bf16_round, synth_rows, table
+from tests.helpers import (bf16_round, fm_exact, hhfm_exact, synth_rows, table,
+                           topk_tie_swaps)
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-5
+# Seeded cases hold at most 2 top-K positions that are fp32 ties (each one
+# verified in float64 by tests/helpers.topk_tie_swaps and reported); all
+# others are index-exact (measured: hhfm K=33 k=64 f32 and the streaming
+# exact-fp32 k=64 K=64 case hold 2 each, every other case 0).
+MAX_TIES = 2
 
 
 def _dev(x):
@@ -121,18 +127,24 @@ def _hhfm_scale(A, E, n_user, n_item):
     return (h @ it.T).max(1, keepdims=True)
 
 
-def _check_topk(ref_scores_full, got_s, got_i, K, scale):
-    rs, ri = orc.top_k(ref_scores_full, K + 1)
-    tol = RTOL * scale
-    mism, amb = orc.topk_index_agreement(rs, ri[:, :K], got_i, tol)
-    assert mism == 0, f"{mism} decidable top-K positions differ (ambiguous {amb})"
-    # every returned score equals the oracle score of the returned item
+def _check_topk(ref_scores_full, got_s, got_i, K, scale, exact):
+    """Top-K parity: indices equal to the oracle's at every position except
+    counted fp32 ties (tests/helpers.TIE_WINDOW, float64 re-scoring); every
+    returned score within 1e-5 of the oracle's score of that item, both
+    relative to the item's own score (elementwise) and to the reduction's
+    magnitude; lists sorted descending.  Returns the tie-swap count."""
+    rs, ri = orc.top_k(ref_scores_full, K)
+    swaps = topk_tie_swaps(got_i, ri, exact)
     picked = np.take_along_axis(ref_scores_full, got_i.astype(np.int64), axis=1)
-    assert np.all(np.abs(picked - got_s) <= tol)
-    # sorted (score desc, idx asc)
+    err = np.abs(picked.astype(np.float64) - got_s)
+    assert np.all(err <= RTOL * scale)
+    rel = err / np.maximum(np.abs(picked), 1e-30)
+    assert rel.max() <= RTOL, f"elementwise relative error {rel.max():.3g}"
     d = np.diff(got_s, axis=1)
     assert np.all(d <= 0)
-    return amb
+    print(f"top-{K}: {swaps} fp32 tie swaps of {got_i.size} positions; max elementwise "
+          f"rel err {rel.max():.3g}, max normwise {float((err / scale).max()):.3g}")
+    return swaps
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
@@ -150,7 +162,8 @@ def test_catalog_topk_hhfm_parity(dtype, k, K):
     s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, n_user, n_item, 0,
                             None, 0, (2, 5), (0, 0))
     ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
-    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, _hhfm_scale(A, E, n_user, n_item))
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, _hhfm_scale(A, E, n_user, n_item),
+                       hhfm_exact(A, E, n_user)) <= MAX_TIES
 
 
 @pytest.mark.parametrize("variant", ["split", "exact", "gemm"])
@@ -178,7 +191,8 @@ def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
     q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
     it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
     scale = (q @ it.T + (q * np.abs(f)).sum(1, keepdims=True)).max(1, keepdims=True) + 0.05
-    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale,
+                       fm_exact(A, E, w, n_user)) <= MAX_TIES
 
 
 @pytest.mark.parametrize("exact", ["0", "1"])
@@ -204,6 +218,7 @@ def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
                                 None, 0, (2, 5), (0, 0))
         ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
         scale = _hhfm_scale(A, E, n_user, n_item)
+        exact = hhfm_exact(A, E, n_user)
     else:
         w = rng.normal(0, 0.01, size=M).astype(np.float32)
         s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_FM, K, n_user, n_item, 0,
@@ -213,7 +228,8 @@ def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
         q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
         it = np.abs(E[n_user:n_user + n_item].astype(np.float64))
         scale = (q @ it.T + (q * np.abs(f)).sum(1, keepdims=True)).max(1, keepdims=True) + 0.05
-    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale)
+        exact = fm_exact(A, E, w, n_user)
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale, exact) <= MAX_TIES
 
 
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
@@ -236,12 +252,14 @@ def test_catalog_topk_small_path_ragged_shard(mode, small, monkeypatch):
     if mode == "hhfm":
         full = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
         scale = _hhfm_scale(A, E, n_user, n_item)
+        exact = hhfm_exact(A, E, n_user)
     else:
         full = orc.fm_catalog_scores(A, E, w, n_user, n_item)
         scale = np.abs(full).max(1, keepdims=True) + 0.05
+        exact = fm_exact(A, E, w, n_user)
     ref = np.full_like(full, -np.inf)
     ref[:, gbase:gbase + cnt] = full[:, gbase:gbase + cnt]
-    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale)
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, scale, exact) <= MAX_TIES
 
 
 def test_catalog_topk_large_catalog_shard_offsets():
@@ -257,7 +275,8 @@ def test_catalog_topk_large_catalog_shard_offsets():
     full = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
     ref = np.full_like(full, -np.inf)
     ref[:, 20000:45000] = full[:, 20000:45000]
-    _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, _hhfm_scale(A, E, n_user, n_item))
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), 20, _hhfm_scale(A, E, n_user, n_item),
+                       hhfm_exact(A, E, n_user)) <= MAX_TIES
 
 
 def test_catalog_topk_ties_lower_index_first():
@@ -288,3 +307,46 @@ def test_topk_merge_device_matches_host():
     ds, di = ops.topk_merge(_dev(sc), _dev(ids))
     assert np.array_equal(hs.numpy(), ds.cpu().numpy())
     assert np.array_equal(hi.numpy(), di.cpu().numpy())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_catalog_topk_c4_shard(dtype, monkeypatch):
+    """configs[3] (C4) per-GPU shape: HHFM k=128, a 1.25M-item shard of a
+    10M-item catalog (rank 3 of 8: global_item_base 3.75M, item rows not at
+    n_user), 1,024 queries, top-20; split-bf16 and exact-fp32 kernels against
+    oracle/cpu_oracle.c (OpenMP, the same k-ordered fp32 arithmetic as
+    OurModel7.py:294 + tf.nn.top_k order) over all 1,024 queries.  Reference
+    path: OurModel7.py:229-307."""
+    from hhfm_amd import ops
+    from oracle import cpu as ocpu
+    rng = np.random.default_rng(3)
+    nu, pre, shard, gbase, k, B, K = 4096, 777, 1_250_000, 3_750_000, 128, 1024, 20
+    M = nu + pre + shard + 12
+    E = rng.standard_normal((M, k), dtype=np.float32)
+    E *= np.float32(0.01)                                     # tf.random_normal(0, 0.01)
+    ctx0 = nu + pre + shard
+    A = np.stack([rng.integers(0, nu, B), np.zeros(B, np.int64),
+                  rng.integers(ctx0, ctx0 + 7, B), rng.integers(ctx0 + 7, ctx0 + 9, B),
+                  rng.integers(ctx0 + 9, ctx0 + 12, B)], 1).astype(np.int32)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    rs, ri = ocpu.catalog_topk(A, E, 1, K, nu + pre, shard, ctx=(2, 5), threads=16)
+    ri = ri + gbase
+    exact = hhfm_exact(A, E, nu + pre - gbase)
+    for variant in ("0", "1"):
+        monkeypatch.setenv("HHFM_CATALOG_EXACT", variant)
+        s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, nu + pre, shard, gbase,
+                                None, 0, (2, 5), (0, 0))
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        swaps = topk_tie_swaps(i, ri, exact)
+        assert i.min() >= gbase and i.max() < gbase + shard
+        # returned scores vs the float64 score of the returned item
+        ex = np.array([exact(b, i[b])[0] for b in range(B)])
+        mag = np.array([exact(b, i[b])[1] for b in range(B)])
+        rel = np.abs(s - ex) / np.abs(ex)
+        assert np.all(np.abs(s - ex) <= RTOL * mag) and rel.max() <= RTOL
+        assert np.all(np.diff(s, axis=1) <= 0)
+        print(f"C4 shard {dtype} exact={variant}: {swaps} fp32 tie swaps of {i.size}; "
+              f"max rel err {rel.max():.3g}")
+        assert swaps <= MAX_TIES   # counted fp32 ties only (each verified above)
