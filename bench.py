@@ -10,15 +10,21 @@ homework] per step and GPU, seed 1 (+rank).
 A step = one hhfm_fm_score_rows launch over the resident batch (inputs in
 HBM before the timed region).  Multi-GPU: one process per GPU, rows sharded
 (weak scaling, no data-path collective); value = all ranks' rows / max time.
+`--gpus N` without a torch.distributed environment re-launches itself under
+torch.distributed.run with N ranks (a child process, started before anything
+touches the GPU); the driver's own torchrun launch takes the same path.
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §Measurement.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -47,13 +53,56 @@ def parse():
                    help="CPU-baseline time budget (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 21)
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
-    p.add_argument("--legs", default="hr,catalog,catalog_bf16,c3",
+    p.add_argument("--legs", default="hr,catalog,catalog_bf16,c3,c5",
                    help="extra legs: hr (HR@10 identity after GPU training on Frappe-shape "
                         "data), catalog / catalog_bf16 (C4 item-sharded top-K over an fp32 / "
                         "bf16 table, RCCL all-gather at N>1), c3 (configs[2]: Frappe-catalog "
-                        "top-20, rank 0)")
+                        "top-20, rank 0), c5 (configs[4]: DeepFM k=256 3x400 bf16 MLP, "
+                        "12.5M rows per GPU)")
     p.add_argument("--hr-epochs", type=int, default=5)
+    p.add_argument("--c5-rows", type=int, default=12_500_000)
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: every rank joins a gloo group and "
+                        "rank 0 prints the world it saw")
     return p.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`--gpus N` outside a torch.distributed environment: run this script
+    under torch.distributed.run with N ranks, one per GPU, as a CHILD process
+    (this process has not touched the GPU), and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args):
+    """Launcher check (no GPU): each rank joins a gloo group; rank 0 prints
+    the ranks it gathered."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    ranks = [rank]
+    if world > 1:
+        dist.init_process_group("gloo")
+        got = [None] * world
+        dist.all_gather_object(got, (rank, int(os.environ.get("LOCAL_RANK", "0"))))
+        ranks = got
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "gpus_arg": args.gpus, "world": world,
+                          "ranks": ranks}), flush=True)
 
 
 def make_batch(rows, n_user, n_item, k, seed, dev):
@@ -75,41 +124,81 @@ def make_batch(rows, n_user, n_item, k, seed, dev):
     return idx, E, w, M
 
 
-def cpu_baseline(idx, E, w, w0, out_gpu, args):
-    """Time the oracle's C restatement (OpenMP) on a bounded sample of the same
-    workload (same table, first cpu_rows rows) on this box's host cores."""
-    from oracle import cpu as ocpu
-    threads = min(len(os.sched_getaffinity(0)), 16)
-    n = min(args.cpu_rows, idx.shape[0])
-    X = idx[:n].cpu().numpy()
-    Eh = E.cpu().numpy()
-    wh = w.cpu().numpy()
-    ref = ocpu.fm_out(X, Eh, wh, w0, threads)          # warm (page-in)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        ocpu.fm_out(X, Eh, wh, w0, threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    m = min(n, 1 << 16)                                 # parity spot-check subset
-    got = out_gpu[:m].cpu().numpy()
-    e = Eh[X[:m].astype(np.int64)].astype(np.float64)
-    scale = (0.5 * (e.sum(1) ** 2 + (e * e).sum(1))).sum(1) + np.abs(wh[X[:m]]).sum(1) + abs(w0)
-    err = float(np.max(np.abs(got - ref[:m]) / scale))
-    cpu_name = platform.processor() or "cpu"
+def _cpu_quota():
+    """Cores the cgroup CPU quota allows (None when unlimited/unreadable)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def _cpu_name():
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
                 if line.startswith("model name"):
-                    cpu_name = line.split(":", 1)[1].strip()
-                    break
+                    return line.split(":", 1)[1].strip()
     except OSError:
         pass
-    return {"value": reps * n / el, "unit": "triples/s", "cores": threads, "kind": "port",
-            "sample": f"{n} rows of the same workload (same 4.3 GB table) x {reps} passes, "
-                      f"oracle/cpu_oracle.c (OpenMP) on {cpu_name}",
-            "gpu_vs_cpu_max_rel_err": err}
+    return platform.processor() or "cpu"
+
+
+def cpu_baseline(idx, E, w, w0, out_gpu, args):
+    """Time the oracle's C restatement of FM.out (oracle/cpu_oracle.c, OpenMP)
+    on this box's host cores over a bounded sample of the same workload (same
+    4.3 GB table, the batch's first rows): one thread, OMP_NUM_THREADS (the
+    box's CPU share), and every core of the affinity mask.  Also the GPU's
+    parity on a subset, elementwise and normwise."""
+    from oracle import cpu as ocpu
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    n = min(args.cpu_rows, idx.shape[0])
+    X = idx[:n].cpu().numpy()
+    Eh = E.cpu().numpy()
+    wh = w.cpu().numpy()
+    ref = ocpu.fm_out(X, Eh, wh, w0, min(share, aff))          # warm (page-in)
+
+    def timed(threads, rows, budget):
+        Xs = X[:rows]
+        ocpu.fm_out(Xs, Eh, wh, w0, threads)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            ocpu.fm_out(Xs, Eh, wh, w0, threads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return reps * rows / el, reps
+    budget = args.cpu_seconds / 3
+    legs = {}
+    r1, reps1 = timed(1, min(n, 1 << 18), budget)
+    legs["1"] = {"threads": 1, "triples_per_s": r1, "rows": min(n, 1 << 18), "passes": reps1}
+    for t in sorted({min(share, aff), aff}):
+        r, reps = timed(t, n, budget)
+        legs[str(t)] = {"threads": t, "triples_per_s": r, "rows": n, "passes": reps}
+    best = max((v for v in legs.values() if v["threads"] > 1), key=lambda v: v["triples_per_s"],
+               default=legs["1"])
+    m = min(n, 1 << 16)                                 # parity spot-check subset
+    got = out_gpu[:m].cpu().numpy().astype(np.float64)
+    rf = ref[:m].astype(np.float64)
+    e = Eh[X[:m].astype(np.int64)].astype(np.float64)
+    scale = (0.5 * (e.sum(1) ** 2 + (e * e).sum(1))).sum(1) + np.abs(wh[X[:m]]).sum(1) + abs(w0)
+    err = np.abs(got - rf)
+    rel = err / np.maximum(np.abs(rf), 1e-30)
+    return {"value": best["triples_per_s"], "unit": "triples/s", "cores": best["threads"],
+            "kind": "port",
+            "sample": f"first {n} rows of the same batch (same 4.3 GB table), "
+                      f"oracle/cpu_oracle.c (OpenMP) on {_cpu_name()}; single thread on "
+                      f"{legs['1']['rows']} rows",
+            "single_thread_triples_per_s": r1, "threads_legs": legs,
+            "affinity_cores": aff, "cgroup_cpu_quota_cores": _cpu_quota(),
+            "gpu_vs_cpu": {"rows": m, "max_rel_err_elementwise": float(rel.max()),
+                           "rows_rel_err_gt_1e-5": int((rel > 1e-5).sum()),
+                           "max_rel_err_normwise": float((err / scale).max()),
+                           "note": "elementwise |gpu-cpu|/|cpu|; rows above 1e-5 are "
+                                   "cancellations ((Σv)²≈Σv², |out| << Σ|terms|), bounded "
+                                   "by the normwise figure"}}
 
 
 def frappe_shape_dataset(path, rows=96203, seed=11):
@@ -214,34 +303,60 @@ def catalog_c3_leg(dev, reps=50):
             "pairs_per_s": pairs / (ms * 1e-3), "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12}
 
 
+ITEM_BLOCK = 1 << 16
+
+
+def item_rows(begin, end, k, dev, seed=3_000_000):
+    """Rows of catalog items [begin, end) as a function of the GLOBAL item
+    index: block j of 65,536 items is drawn from its own seeded generator, so
+    every rank count N builds the same catalog and the top-K must match."""
+    out = torch.empty(end - begin, k, device=dev)
+    j = begin // ITEM_BLOCK
+    while j * ITEM_BLOCK < end:
+        b0, b1 = j * ITEM_BLOCK, (j + 1) * ITEM_BLOCK
+        g = torch.Generator(device=dev)
+        g.manual_seed(seed + j)
+        blk = torch.empty(ITEM_BLOCK, k, device=dev).normal_(0, 0.01, generator=g)
+        lo, hi = max(b0, begin), min(b1, end)
+        out[lo - begin:hi - begin] = blk[lo - b0:hi - b0]
+        j += 1
+    return out
+
+
+def _sha(t):
+    return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()[:16]
+
+
 def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
     """C4: HHFM k=128, 1 M users, 10 M items sharded contiguously over the
     ranks, 1,024 queries, K=20, fp32 (or bf16) table; local
-    hhfm_catalog_topk + RCCL all-gather + hhfm_topk_merge per step."""
+    hhfm_catalog_topk + one packed RCCL all-gather + hhfm_topk_merge per step.
+    Table per rank: [users | 12 ctx | this rank's items]; the catalog is a
+    function of the global item index (item_rows), so the top-20 checksum is
+    the same for every N."""
     from hhfm_amd import distributed as hd
     from hhfm_amd import ops
     nu, ni, k, B, K = 1 << 20, 10_000_000, 128, 1024, 20
     begin, end = hd.shard_range(ni, world, rank)
     g = torch.Generator(device=dev)
     g.manual_seed(3)
-    # replicated users + ctx, only this rank's item rows are materialised
     rows_user = torch.empty(nu, k, device=dev).normal_(0, 0.01, generator=g)
     rows_ctx = torch.empty(12, k, device=dev).normal_(0, 0.01, generator=g)
-    gi = torch.Generator(device=dev)
-    gi.manual_seed(1000 + rank)
-    rows_item = torch.empty(end - begin, k, device=dev).normal_(0, 0.01, generator=gi)
-    E = torch.cat([rows_user, rows_item, rows_ctx]).to(table_dtype).contiguous()
-    del rows_user, rows_item
-    off = nu + (end - begin)
+    E = torch.cat([rows_user, rows_ctx, item_rows(begin, end, k, dev)]).to(table_dtype)
+    E = E.contiguous()
+    del rows_user
     cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
             torch.zeros(B, dtype=torch.int64, device=dev)]
+    off = nu
     for c in (7, 2, 3):
-        cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
+        cols.append(torch.randint(0, c, (B,), generator=g, device=dev) + off)
         off += c
     A = torch.stack(cols, 1).to(torch.int32).contiguous()
+    row0 = nu + 12                       # this rank's first item row
 
     def scorer(A_, b0, cnt, Kl):
-        return ops.catalog_topk(A_, E, ops.MODE_HHFM, Kl, nu, cnt, b0, None, 0, (2, 5), (0, 0))
+        return ops.catalog_topk(A_, E, ops.MODE_HHFM, Kl, row0 + (b0 - begin), cnt, b0, None,
+                                0, (2, 5), (0, 0))
 
     def step():
         return hd.sharded_topk(A, K, ni, scorer)
@@ -263,22 +378,110 @@ def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
     pairs = B * ni
     tname = "fp32" if table_dtype == torch.float32 else "bf16"
     return {"workload": f"C4: HHFM k=128 {tname} table, 10M-item catalog sharded over ranks, "
-                        "1,024 queries, top-20 (local split-bf16 MFMA score + select, RCCL "
-                        "all-gather, merge)",
+                        "1,024 queries, top-20 (local split-bf16 MFMA score + select, one "
+                        "packed RCCL all-gather, merge)",
             "ms_per_query_batch": ms, "pairs_per_s": pairs / (ms * 1e-3),
-            "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world}
+            "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world,
+            "top20_ids_sha256": _sha(i), "top20_scores_sha256": _sha(s),
+            "checksum_note": "catalog seeded by global item index: identical for every N"}
+
+
+def c5_leg(dev, world, rank, rows, reps=3):
+    """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137) on the
+    fused bf16-MFMA kernel, Frappe vocabulary, `rows` rows per GPU (12.5M =
+    the 100M-row job over 8 GPUs; weak scaling, rows sharded, no collective)."""
+    from hhfm_amd import ops
+    from hhfm_amd.DFM import DeepFM
+    nu, ni, ctx = 957, 4082, (7, 2, 3)
+    M = nu + ni + sum(ctx)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4 + rank)
+    cols = [torch.randint(0, nu, (rows,), generator=g, device=dev),
+            torch.randint(nu, nu + ni, (rows,), generator=g, device=dev)]
+    off = nu + ni
+    for c in ctx:
+        cols.append(torch.randint(off, off + c, (rows,), generator=g, device=dev))
+        off += c
+    X = torch.stack(cols, 1).to(torch.int32).contiguous()
+    del cols
+    m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
+               mlp_dtype=torch.bfloat16)
+    Wt, bs, dims, Wp, bp = m._prepared()
+    out = torch.empty(rows, device=dev)
+    wb = m.weights["feature_bias"].reshape(-1)
+
+    def step():
+        ops.dfm_forward(X, m.table, wb, Wt, bs, dims, torch.bfloat16, Wp, bp, out=out)
+
+    step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    evs = []
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    ms = float(t[0]) / reps * 1e3
+    kern = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    fl = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
+    return {"workload": "C5 (configs[4]): DeepFM F=5 k=256 + MLP 3x400 (bf16 MFMA, fp32 "
+                        "table and accumulation), Frappe vocabulary, rows sharded "
+                        f"{rows:,} per GPU", "ranks": world,
+            "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
+            "roofline": {"bound": "mfma", "flops_per_row": fl,
+                         "achieved_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
+                         "peak_TFLOPs": 2500.0,
+                         "frac": fl * rows / (kern * 1e-3) / 1e12 / 2500.0}}
+
+
+def stream_read_peak(buf, reps=5):
+    """The box's measured HBM read ceiling: hhfm_probe_stream_read (one
+    16-B-per-lane sequential pass) over `buf`, best of `reps`, GB/s."""
+    from hhfm_amd._native import native
+    dev = buf.device
+    sink = torch.zeros(1, device=dev)
+    nbytes = (buf.numel() * buf.element_size()) & ~15
+    st = torch.cuda.current_stream(dev).cuda_stream
+    native().probe_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), st)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        native().probe_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), st)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    return nbytes / (best * 1e-3) / 1e9
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))       # before anything touches the GPU
+    if args.dry_run:
+        dry_run(args)
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    rccl_world = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
+        rccl_world = dist.get_world_size()
     from hhfm_amd import ops
 
     idx, E, w, M = make_batch(args.rows, args.users, args.items, args.k, 1 + rank, dev)
@@ -319,6 +522,12 @@ def main():
     bpr = 2 * args.k * 4 + 5 * 4 + 2 * 4 + 4
     bpr_survey = 5 * args.k * 4 + 5 * 4 + 5 * 4 + 4
     achieved = bpr * args.rows / (kern_ms * 1e-3) / 1e9
+    # K1 issues 128-B HBM requests only (TCC_EA0_RDREQ_32B = 0 for every cache
+    # policy of the 4-B `w` gathers; profiles/r02_k1_wpolicy.json): the bytes
+    # that cross HBM at that granularity are 2 rows x 256 B + 2 w lines x 128 B
+    # + ids + out = 792 B/row at k=64.
+    bpr_lines = 2 * args.k * 4 + 2 * 128 + 5 * 4 + 4
+    peak_meas = stream_read_peak(E)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -332,6 +541,8 @@ def main():
 
     result = {
         "metric": METRIC, "value": value, "unit": "triples/s", "n_gpus": world,
+        "world": {"ranks": world, "gpus_arg": args.gpus, "rccl_world_size": rccl_world,
+                  "backend": "nccl (RCCL)" if world > 1 else None},
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
@@ -348,7 +559,18 @@ def main():
                                      if traffic else None,
                      "algorithmic_bytes_per_row": bpr,
                      "survey_bytes_per_row": bpr_survey,
-                     "survey_rate_GBps": bpr_survey * args.rows / (kern_ms * 1e-3) / 1e9},
+                     "survey_rate_GBps": bpr_survey * args.rows / (kern_ms * 1e-3) / 1e9,
+                     "peak_measured": peak_meas,
+                     "peak_measured_how": "hhfm_probe_stream_read: one sequential 16-B/lane "
+                                          "read of the 4.3 GB table, best of 5, this box",
+                     "frac_vs_measured": (achieved / peak_meas) if peak_meas else None,
+                     "line_bytes_per_row": bpr_lines,
+                     "line_rate_GBps": bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9,
+                     "line_frac_vs_measured": (bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9
+                                               / peak_meas) if peak_meas else None,
+                     "traffic_source": "calibrated, not measured in this run: PMC bytes/row "
+                                       "from profiles/traffic_fm_rows.json (separate "
+                                       "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes) x rows"},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(idx, E, w, w0, out, args)
@@ -373,6 +595,12 @@ def main():
             extra["catalog_c4_bf16"] = catalog_leg(dev, world, rank, table_dtype=torch.bfloat16)
         except Exception as e:  # noqa: BLE001
             extra["catalog_c4_bf16"] = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+    if "c5" in legs:
+        try:
+            extra["dfm_c5"] = c5_leg(dev, world, rank, args.c5_rows)
+        except Exception as e:  # noqa: BLE001
+            extra["dfm_c5"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
     if "hr" in legs and rank == 0:
         try:

@@ -77,15 +77,31 @@ class ScoringModel(object):
 
     # -- conversions ----------------------------------------------------------
     def _idx(self, X) -> torch.Tensor:
+        """Ids -> device int32.  Wider integer inputs are range-checked BEFORE
+        narrowing (a cast would wrap 2**32+5 to 5 and slip past the check)."""
+        checked = False
         if isinstance(X, torch.Tensor):
+            if X.dtype != torch.int32 and self.validate and X.numel():
+                lo, hi = int(X.min()), int(X.max())
+                if lo < 0 or hi >= self.features_M:
+                    raise ValueError(f"indices must be in [0, {self.features_M}), "
+                                     f"got [{lo}, {hi}]")
+                checked = True
             t = X.to(device=self.device, dtype=torch.int32)
         else:
-            t = torch.from_numpy(np.ascontiguousarray(np.asarray(X), dtype=np.int32))
+            a = np.asarray(X)
+            if a.dtype != np.int32 and self.validate and a.size:
+                lo, hi = int(a.min()), int(a.max())
+                if lo < 0 or hi >= self.features_M:
+                    raise ValueError(f"indices must be in [0, {self.features_M}), "
+                                     f"got [{lo}, {hi}]")
+                checked = True
+            t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int32))
             t = t.to(self.device, non_blocking=False)
         if t.dim() != 2:
             raise ValueError("expected a 2-D index matrix [rows, columns]")
         t = t.contiguous()
-        if self.validate:
+        if self.validate and not checked:
             ops.validate_ids(t, self.features_M)
         return t
 

@@ -790,6 +790,19 @@ extern "C" int hhfm_catalog_topk(
     int32_t dtype, const float* w, int32_t item_row_begin, int32_t item_count,
     int32_t global_item_base, int32_t K, float* top_score, int32_t* top_idx,
     void* workspace, size_t ws_bytes, void* stream) {
+  return hhfm_catalog_topk_ex(qidx, B, ncols, mode, user_col, ctx_begin, ctx_end, time_begin,
+                              time_end, E, features_M, k, dtype, w, item_row_begin, item_count,
+                              global_item_base, K, top_score, top_idx, workspace, ws_bytes,
+                              nullptr, stream);
+}
+
+extern "C" int hhfm_catalog_topk_ex(
+    const int32_t* qidx, int64_t B, int32_t ncols, int32_t mode,
+    int32_t user_col, int32_t ctx_begin, int32_t ctx_end, int32_t time_begin,
+    int32_t time_end, const void* E, int64_t features_M, int32_t k,
+    int32_t dtype, const float* w, int32_t item_row_begin, int32_t item_count,
+    int32_t global_item_base, int32_t K, float* top_score, int32_t* top_idx,
+    void* workspace, size_t ws_bytes, int32_t* status, void* stream) {
   if (B < 0 || ncols < 1 || ncols > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (mode != HHFM_MODE_FM && mode != HHFM_MODE_HHFM) return HHFM_EINVAL;
@@ -822,6 +835,11 @@ extern "C" int hhfm_catalog_topk(
   const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
   if (me != hipSuccess) return (int)me;
   const char* Eb = reinterpret_cast<const char*>(E);
+  {
+    const int rc = launch_check_query_ids(qidx, B, ncols, user_col, ctx_begin, ctx_end,
+                                          time_begin, time_end, features_M, status, st);
+    if (rc != HHFM_OK) return rc;
+  }
 
   {
     int64_t blocks = (p.Bpad + 3) / 4;

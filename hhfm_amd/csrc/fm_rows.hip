@@ -40,10 +40,25 @@ HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
 // ---------------------------------------------------------------------------
 // FM row kernel: out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0
 // ---------------------------------------------------------------------------
-template <int F, int LPR, bool BF16, bool HAS_W, bool NT>
+// w[id] load.  WAUX < 0: plain global load (default).  WAUX >= 0: a buffer
+// load with that cache-policy operand (bit 0 sc0, bit 1 nt, bit 4 sc1) —
+// measurement variants for the 4-B `w` gathers.
+template <int WAUX>
+HHFM_DEV float load_w(const float* __restrict__ w, int32_t id, int64_t M) {
+  if constexpr (WAUX < 0) {
+    return w[id];
+  } else {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(w), (short)0, (int)(M * 4), 0x00020000);
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, id * 4, 0, WAUX));
+  }
+}
+
+template <int F, int LPR, bool BF16, bool HAS_W, bool NT, int WAUX = -1>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
-    int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out) {
+    int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out,
+    int32_t* __restrict__ status) {
   constexpr int U = RowsPerLane<F>::value;
   constexpr int RPW = kWave / LPR;  // rows per wave per unroll slot
   constexpr int RPI = RPW * U;      // rows per wave-iteration
@@ -59,6 +74,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
 
   int64_t base = wave * RPI;
   int32_t raw[U][F];
+  bool bad = false;
   if (base < B) load_ids<F, U, NT>(raw, idx, base, B, g, RPW, F);
 
   for (; base < B; base += stride) {
@@ -69,6 +85,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
 #pragma unroll
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
+        bad |= id[u][f] != raw[u][f];
         c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
@@ -86,7 +103,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
           int32_t my = id[u][0];
 #pragma unroll
           for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
-          const float wl = w[my];
+          const float wl = load_w<WAUX>(w, my, M);
           wv[u] += (fsel < F) ? wl : 0.f;
         }
       }
@@ -120,6 +137,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
       }
     }
   }
+  report_bad_id(status, bad);
 }
 
 // Generic fallback (any k, any F <= 64): one wave per row, lanes stride over k.
@@ -127,13 +145,15 @@ template <bool BF16>
 __global__ __launch_bounds__(256) void fm_rows_generic(
     const int32_t* __restrict__ idx, int64_t B, int F, const char* __restrict__ E,
     int64_t M, int k, const float* __restrict__ w, float w0,
-    float* __restrict__ out) {
+    float* __restrict__ out, int32_t* __restrict__ status) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
   const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
   const int esz = BF16 ? 2 : 4;
+  bool bad = false;
   for (int64_t row = wave; row < B; row += nwave) {
     const int32_t* p = idx + row * (int64_t)F;
+    for (int f = lane; f < F; f += kWave) bad |= clamp_id(p[f], M) != p[f];
     float t = 0.f;
     for (int e = lane; e < k; e += kWave) {
       float s = 0.f, q = 0.f;
@@ -152,6 +172,7 @@ __global__ __launch_bounds__(256) void fm_rows_generic(
       for (int f = 0; f < F; ++f) fb += w[clamp_id(p[f], M)];
     if (lane == 0) out[row] = (t + fb) + w0;
   }
+  report_bad_id(status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -161,7 +182,8 @@ __global__ __launch_bounds__(256) void fm_rows_generic(
 template <int F, int LPR, bool BF16>
 __global__ __launch_bounds__(256) void hybrid_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, int nctx,
-    const char* __restrict__ E, int64_t M, float* __restrict__ out) {
+    const char* __restrict__ E, int64_t M, float* __restrict__ out,
+    int32_t* __restrict__ status) {
   constexpr int U = RowsPerLane<F>::value;
   constexpr int RPW = kWave / LPR;
   constexpr int RPI = RPW * U;
@@ -178,6 +200,7 @@ __global__ __launch_bounds__(256) void hybrid_rows_fast(
 
   int64_t base = wave * RPI;
   int32_t raw[U][F];
+  bool bad = false;
   if (base < B) load_ids<F, U>(raw, idx, base, B, g, RPW, F);
 
   for (; base < B; base += stride) {
@@ -188,6 +211,7 @@ __global__ __launch_bounds__(256) void hybrid_rows_fast(
 #pragma unroll
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
+        bad |= id[u][f] != raw[u][f];
         c[u][f].load(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
@@ -215,13 +239,14 @@ __global__ __launch_bounds__(256) void hybrid_rows_fast(
       if (sub == 0 && row < B) out[row] = t;
     }
   }
+  report_bad_id(status, bad);
 }
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void hybrid_rows_generic(
     const int32_t* __restrict__ idx, int64_t B, int ncols, int ucol, int icol,
     int c0, int c1, int t0, int t1, const char* __restrict__ E, int64_t M,
-    int k, float* __restrict__ out) {
+    int k, float* __restrict__ out, int32_t* __restrict__ status) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
   const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
@@ -231,8 +256,10 @@ __global__ __launch_bounds__(256) void hybrid_rows_generic(
     return BF16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(r)[e])
                 : reinterpret_cast<const float*>(r)[e];
   };
+  bool bad = false;
   for (int64_t row = wave; row < B; row += nwave) {
     const int32_t* p = idx + row * (int64_t)ncols;
+    for (int c = lane; c < ncols; c += kWave) bad |= clamp_id(p[c], M) != p[c];
     float t = 0.f;
     for (int e = lane; e < k; e += kWave) {
       float h = val(p[ucol], e);
@@ -251,6 +278,7 @@ __global__ __launch_bounds__(256) void hybrid_rows_generic(
     t = group_sum<kWave>(t);
     if (lane == 0) out[row] = t;
   }
+  report_bad_id(status, bad);
 }
 
 // ---------------------------------------------------------------------------
@@ -264,31 +292,57 @@ static int grid_for(int64_t rows, int64_t rows_per_block) {
   return (int)g;
 }
 
+// Measurement variants of the configs[1] shape (F=5, k=64 fp32, with w):
+// flag bits 4..7 select the cache policy of the `w` gathers.
+static bool launch_fm_wpolicy(int sel, const int32_t* idx, int64_t B, const char* E,
+                              int64_t M, const float* w, float w0, float* out,
+                              int32_t* status, hipStream_t s) {
+  constexpr int RPB = 4 * (kWave / 16) * RowsPerLane<5>::value;
+  const int grid = grid_for(B, RPB);
+#define HHFM_WPOL(SEL, AUX)                                                        \
+  case SEL:                                                                        \
+    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, AUX>), dim3(grid), \
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);         \
+    return true;
+  switch (sel) {
+    HHFM_WPOL(1, 0)
+    HHFM_WPOL(2, 1)
+    HHFM_WPOL(3, 2)
+    HHFM_WPOL(4, 3)
+    HHFM_WPOL(5, 16)
+    HHFM_WPOL(6, 17)
+    HHFM_WPOL(7, 18)
+    HHFM_WPOL(8, 19)
+    default: return false;
+  }
+#undef HHFM_WPOL
+}
+
 template <int F, int LPR, bool BF16>
 static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            int64_t M, const float* w, float w0, float* out,
-                           bool nt, hipStream_t s) {
+                           bool nt, int32_t* status, hipStream_t s) {
   constexpr int RPB = 4 * (kWave / LPR) * RowsPerLane<F>::value;
   const int grid = grid_for(B, RPB);
   if (w && nt)
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, true>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else if (w)
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, false>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, false>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
 }
 
 template <int F, int LPR, bool BF16>
 static void launch_hybrid_fast(const int32_t* idx, int64_t B, int nctx,
                                const char* E, int64_t M, float* out,
-                               hipStream_t s) {
+                               int32_t* status, hipStream_t s) {
   constexpr int RPB = 4 * (kWave / LPR) * RowsPerLane<F>::value;
   const int grid = grid_for(B, RPB);
   hipLaunchKernelGGL((hybrid_rows_fast<F, LPR, BF16>), dim3(grid), dim3(256), 0,
-                     s, idx, B, nctx, E, M, out);
+                     s, idx, B, nctx, E, M, out, status);
 }
 
 // dispatch on LPR (16-byte chunks per row) for a fixed F and dtype
@@ -318,22 +372,22 @@ static void launch_hybrid_fast(const int32_t* idx, int64_t B, int nctx,
 
 static bool try_fm_fast(const int32_t* idx, int64_t B, int F, const char* E,
                         int64_t M, int lpr, bool bf16, const float* w, float w0,
-                        float* out, bool nt, hipStream_t s) {
+                        float* out, bool nt, int32_t* status, hipStream_t s) {
   if (bf16) {
-    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, nt, s)
+    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, nt, status, s)
   } else {
-    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, nt, s)
+    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, nt, status, s)
   }
   return true;
 }
 
 static bool try_hybrid_fast(const int32_t* idx, int64_t B, int F, int nctx,
                             const char* E, int64_t M, int lpr, bool bf16,
-                            float* out, hipStream_t s) {
+                            float* out, int32_t* status, hipStream_t s) {
   if (bf16) {
-    HHFM_F_SWITCH(launch_hybrid_fast, true, idx, B, nctx, E, M, out, s)
+    HHFM_F_SWITCH(launch_hybrid_fast, true, idx, B, nctx, E, M, out, status, s)
   } else {
-    HHFM_F_SWITCH(launch_hybrid_fast, false, idx, B, nctx, E, M, out, s)
+    HHFM_F_SWITCH(launch_hybrid_fast, false, idx, B, nctx, E, M, out, status, s)
   }
   return true;
 }
@@ -351,7 +405,8 @@ using namespace hhfm;
 extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
                                      const void* E, int64_t features_M, int32_t k,
                                      int32_t dtype, const float* w, float w0,
-                                     float* out, int32_t flags, void* stream) {
+                                     float* out, int32_t flags, int32_t* status,
+                                     void* stream) {
   if (B < 0 || F < 1 || F > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (B == 0) return HHFM_OK;
@@ -360,18 +415,24 @@ extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
   const bool bf16 = dtype == HHFM_BF16;
   const int lpr = lpr_for(k, dtype);
   const bool aligned = (reinterpret_cast<uintptr_t>(E) & 15) == 0;
+  const int wsel = (flags >> 4) & 15;
+  if (wsel && F == 5 && lpr == 16 && !bf16 && aligned && w && features_M < (1LL << 29) &&
+      launch_fm_wpolicy(wsel, idx, B, reinterpret_cast<const char*>(E), features_M, w, w0,
+                        out, status, s))
+    return (int)hipGetLastError();
   if (!(lpr && aligned &&
         try_fm_fast(idx, B, F, reinterpret_cast<const char*>(E), features_M,
-                    lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0, s))) {
+                    lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0, status,
+                    s))) {
     const int grid = grid_for(B, 4);
     if (bf16)
       hipLaunchKernelGGL(fm_rows_generic<true>, dim3(grid), dim3(256), 0, s, idx,
                          B, F, reinterpret_cast<const char*>(E), features_M, k,
-                         w, w0, out);
+                         w, w0, out, status);
     else
       hipLaunchKernelGGL(fm_rows_generic<false>, dim3(grid), dim3(256), 0, s,
                          idx, B, F, reinterpret_cast<const char*>(E),
-                         features_M, k, w, w0, out);
+                         features_M, k, w, w0, out, status);
   }
   return (int)hipGetLastError();
 }
@@ -381,16 +442,17 @@ extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                                   int32_t dtype, const float* w, float w0,
                                   float* out, void* stream) {
   return hhfm_fm_score_rows_ex(idx, B, F, E, features_M, k, dtype, w, w0, out,
-                               HHFM_FM_ROWS_DEFAULT_FLAGS, stream);
+                               HHFM_FM_ROWS_DEFAULT_FLAGS, nullptr, stream);
 }
 
-extern "C" int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B,
-                                      int32_t ncols, int32_t user_col,
-                                      int32_t item_col, int32_t ctx_begin,
-                                      int32_t ctx_end, int32_t time_begin,
-                                      int32_t time_end, const void* E,
-                                      int64_t features_M, int32_t k,
-                                      int32_t dtype, float* out, void* stream) {
+extern "C" int hhfm_hybrid_score_rows_ex(const int32_t* idx, int64_t B,
+                                         int32_t ncols, int32_t user_col,
+                                         int32_t item_col, int32_t ctx_begin,
+                                         int32_t ctx_end, int32_t time_begin,
+                                         int32_t time_end, const void* E,
+                                         int64_t features_M, int32_t k,
+                                         int32_t dtype, float* out, int32_t* status,
+                                         void* stream) {
   if (B < 0 || ncols < 2 || ncols > 64 || k < 1 || features_M < 1)
     return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
@@ -417,20 +479,32 @@ extern "C" int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B,
   if (!(canonical && lpr && aligned &&
         try_hybrid_fast(idx, B, ncols, nctx,
                         reinterpret_cast<const char*>(E), features_M, lpr,
-                        bf16, out, s))) {
+                        bf16, out, status, s))) {
     const int grid = grid_for(B, 4);
     if (bf16)
       hipLaunchKernelGGL(hybrid_rows_generic<true>, dim3(grid), dim3(256), 0, s,
                          idx, B, ncols, user_col, item_col, ctx_begin, ctx_end,
                          time_begin, time_end,
-                         reinterpret_cast<const char*>(E), features_M, k, out);
+                         reinterpret_cast<const char*>(E), features_M, k, out, status);
     else
       hipLaunchKernelGGL(hybrid_rows_generic<false>, dim3(grid), dim3(256), 0,
                          s, idx, B, ncols, user_col, item_col, ctx_begin,
                          ctx_end, time_begin, time_end,
-                         reinterpret_cast<const char*>(E), features_M, k, out);
+                         reinterpret_cast<const char*>(E), features_M, k, out, status);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B,
+                                      int32_t ncols, int32_t user_col,
+                                      int32_t item_col, int32_t ctx_begin,
+                                      int32_t ctx_end, int32_t time_begin,
+                                      int32_t time_end, const void* E,
+                                      int64_t features_M, int32_t k,
+                                      int32_t dtype, float* out, void* stream) {
+  return hhfm_hybrid_score_rows_ex(idx, B, ncols, user_col, item_col, ctx_begin, ctx_end,
+                                   time_begin, time_end, E, features_M, k, dtype, out,
+                                   nullptr, stream);
 }
 
 extern "C" const char* hhfm_error_string(int code) {

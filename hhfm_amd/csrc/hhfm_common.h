@@ -70,6 +70,21 @@ HHFM_DEV int32_t clamp_id(int32_t id, int64_t M) {
   return (uint64_t)(uint32_t)id < (uint64_t)M ? id : 0;
 }
 
+// Record that this wave met an id outside [0, M) in the caller's status word
+// (include/hhfm.h, HHFM_STATUS_BAD_ID): one vector atomic per wave that saw
+// one, none otherwise; NULL = the caller did not ask.  Every lane of the wave
+// must call it (kernel epilogue).
+HHFM_DEV void report_bad_id(int32_t* status, bool bad) {
+  if (status == nullptr) return;
+  const uint64_t m = __ballot(bad);
+  if (m != 0 && (threadIdx.x & (kWave - 1)) == (unsigned)(__ffsll((long long)m) - 1))
+    atomicOr(status, HHFM_STATUS_BAD_ID);
+}
+
+// Query-column id check of hhfm_catalog_topk_ex (status.hip).
+int launch_check_query_ids(const int32_t* q, int64_t B, int ncols, int ucol, int c0, int c1,
+                           int t0, int t1, int64_t M, int32_t* status, hipStream_t s);
+
 // Butterfly sum over aligned groups of G lanes (G a power of two <= 64).
 template <int G>
 HHFM_DEV float group_sum(float x) {

@@ -56,13 +56,14 @@ PYBIND11_MODULE(_hhfm, m) {
 
   m.def("fm_score_rows_ex",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype,
-           uptr w, float w0, uptr out, int flags, uptr stream) {
+           uptr w, float w0, uptr out, int flags, uptr status, uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
             rc = hhfm_fm_score_rows_ex(P<const int32_t>(idx), B, F, P<const void>(E),
                                        M, k, dtype, P<const float>(w), w0,
-                                       P<float>(out), flags, P<void>(stream));
+                                       P<float>(out), flags, P<int32_t>(status),
+                                       P<void>(stream));
           }
           check(rc, "hhfm_fm_score_rows_ex");
         });
@@ -70,16 +71,16 @@ PYBIND11_MODULE(_hhfm, m) {
   m.def("hybrid_score_rows",
         [](uptr idx, int64_t B, int ncols, int ucol, int icol, int c0, int c1,
            int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr out,
-           uptr stream) {
+           uptr status, uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_hybrid_score_rows(P<const int32_t>(idx), B, ncols, ucol,
-                                        icol, c0, c1, t0, t1, P<const void>(E),
-                                        M, k, dtype, P<float>(out),
-                                        P<void>(stream));
+            rc = hhfm_hybrid_score_rows_ex(P<const int32_t>(idx), B, ncols, ucol,
+                                           icol, c0, c1, t0, t1, P<const void>(E),
+                                           M, k, dtype, P<float>(out), P<int32_t>(status),
+                                           P<void>(stream));
           }
-          check(rc, "hhfm_hybrid_score_rows");
+          check(rc, "hhfm_hybrid_score_rows_ex");
         });
 
   m.def("catalog_topk_workspace",
@@ -94,20 +95,49 @@ PYBIND11_MODULE(_hhfm, m) {
         [](uptr qidx, int64_t B, int ncols, int mode, int ucol, int c0, int c1,
            int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr w,
            int item_row_begin, int item_count, int global_item_base, int K,
-           uptr top_score, uptr top_idx, uptr ws, size_t ws_bytes,
+           uptr top_score, uptr top_idx, uptr ws, size_t ws_bytes, uptr status,
            uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_catalog_topk(
+            rc = hhfm_catalog_topk_ex(
                 P<const int32_t>(qidx), B, ncols, mode, ucol, c0, c1, t0, t1,
                 P<const void>(E), M, k, dtype, P<const float>(w),
                 item_row_begin, item_count, global_item_base, K,
                 P<float>(top_score), P<int32_t>(top_idx), P<void>(ws), ws_bytes,
-                P<void>(stream));
+                P<int32_t>(status), P<void>(stream));
           }
-          check(rc, "hhfm_catalog_topk");
+          check(rc, "hhfm_catalog_topk_ex");
         });
+
+  m.def("check_ids", [](uptr idx, int64_t n, int64_t M, uptr status, uptr stream) {
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = hhfm_check_ids(P<const int32_t>(idx), n, M, P<int32_t>(status), P<void>(stream));
+    }
+    check(rc, "hhfm_check_ids");
+  });
+
+  // returns HHFM_OK / HHFM_EINVAL as an int (the caller raises with its own message)
+  m.def("status_read", [](uptr status, uptr stream) {
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = hhfm_status_read(P<int32_t>(status), P<void>(stream));
+    }
+    if (rc != HHFM_OK && rc != HHFM_EINVAL) check(rc, "hhfm_status_read");
+    return rc;
+  });
+
+  m.def("probe_stream_read", [](uptr buf, int64_t bytes, uptr sink, uptr stream) {
+    int rc;
+    {
+      py::gil_scoped_release nogil;
+      rc = hhfm_probe_stream_read(P<const void>(buf), bytes, P<float>(sink), P<void>(stream));
+    }
+    check(rc, "hhfm_probe_stream_read");
+  });
 
   m.def("pf_contains",
         [](uptr keys, int64_t nkeys, int key_cols, uptr codes, int64_t ncodes, uptr rows,

@@ -52,19 +52,50 @@ def _idx(t: torch.Tensor, name: str) -> torch.Tensor:
     return t
 
 
+_STATUS = {}
+
+
+def status_word(dev: torch.device) -> torch.Tensor:
+    """This device's id status word (include/hhfm.h HHFM_STATUS_BAD_ID)."""
+    t = _STATUS.get(dev.index)
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int32, device=dev)
+        _STATUS[dev.index] = t
+    return t
+
+
+def check_status(dev: torch.device, features_M: int) -> None:
+    """Synchronise and raise like tf.nn.embedding_lookup (InvalidArgumentError,
+    FM.py:99) if a kernel on this stream met an id outside [0, features_M)."""
+    if native().status_read(status_word(dev).data_ptr(), _stream(dev)) != 0:
+        raise ValueError(f"indices must be in [0, {features_M})")
+
+
 def validate_ids(idx: torch.Tensor, features_M: int) -> None:
-    """Raise like tf.nn.embedding_lookup does for ids outside [0, M).
-    (The kernels clamp such ids to row 0 so they can never fault.)"""
+    """Raise like tf.nn.embedding_lookup does for ids outside [0, M): one
+    hhfm_check_ids kernel + a 4-byte status read (the kernels themselves read
+    such ids as row 0, so they can never fault)."""
     if idx.numel() == 0:
         return
-    lo, hi = int(idx.min()), int(idx.max())
-    if lo < 0 or hi >= features_M:
-        raise ValueError(f"indices must be in [0, {features_M}), got [{lo}, {hi}]")
+    dev = _need_cuda(idx)
+    native().check_ids(idx.data_ptr(), idx.numel(), int(features_M),
+                       status_word(dev).data_ptr(), _stream(dev))
+    check_status(dev, features_M)
+
+
+def _status_ptr(status: Optional[torch.Tensor]) -> int:
+    if status is None:
+        return 0
+    if status.dtype != torch.int32 or status.numel() < 1 or not status.is_cuda:
+        raise TypeError("status must be a device int32 tensor")
+    return status.data_ptr()
 
 
 def fm_score_rows(idx: torch.Tensor, E: torch.Tensor, w: Optional[torch.Tensor],
-                  w0: float = 0.0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """FM.out (FM.py:99-120) for rows ``idx`` [B, F] -> float32 [B]."""
+                  w0: float = 0.0, out: Optional[torch.Tensor] = None,
+                  status: Optional[torch.Tensor] = None, flags: int = 0) -> torch.Tensor:
+    """FM.out (FM.py:99-120) for rows ``idx`` [B, F] -> float32 [B].
+    ``status``: optional device int32 word the kernel flags bad ids in."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, out)
     B, F = idx.shape
@@ -73,16 +104,17 @@ def fm_score_rows(idx: torch.Tensor, E: torch.Tensor, w: Optional[torch.Tensor],
         raise ValueError("w must be float32 with features_M entries")
     if out is None:
         out = torch.empty(B, dtype=torch.float32, device=dev)
-    native().fm_score_rows(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E),
-                           0 if w is None else w.data_ptr(), float(w0),
-                           out.data_ptr(), _stream(dev))
+    native().fm_score_rows_ex(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E),
+                              0 if w is None else w.data_ptr(), float(w0),
+                              out.data_ptr(), int(flags), _status_ptr(status), _stream(dev))
     return out
 
 
 def hybrid_score_rows(idx: torch.Tensor, E: torch.Tensor, user_col: int = 0,
                       item_col: int = 1, ctx: Tuple[int, int] = (0, 0),
                       time: Tuple[int, int] = (0, 0),
-                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                      out: Optional[torch.Tensor] = None,
+                      status: Optional[torch.Tensor] = None) -> torch.Tensor:
     """OUR.PositiveFeadback (OurModel7.py:105-171) for rows ``idx`` -> [B]."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, out)
@@ -92,7 +124,8 @@ def hybrid_score_rows(idx: torch.Tensor, E: torch.Tensor, user_col: int = 0,
         out = torch.empty(B, dtype=torch.float32, device=dev)
     native().hybrid_score_rows(idx.data_ptr(), B, ncols, user_col, item_col,
                                ctx[0], ctx[1], time[0], time[1], E.data_ptr(), M, k,
-                               _dtype_code(E), out.data_ptr(), _stream(dev))
+                               _dtype_code(E), out.data_ptr(), _status_ptr(status),
+                               _stream(dev))
     return out
 
 
@@ -111,7 +144,8 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
 def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
                  item_row_begin: int, item_count: int, global_item_base: int = 0,
                  w: Optional[torch.Tensor] = None, user_col: int = 0,
-                 ctx: Tuple[int, int] = (0, 0), time: Tuple[int, int] = (0, 0)
+                 ctx: Tuple[int, int] = (0, 0), time: Tuple[int, int] = (0, 0),
+                 status: Optional[torch.Tensor] = None
                  ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Full-catalog score + top-K (FM.topk FM.py:172-198, OUR.topk
     OurModel7.py:229-307). Returns (scores float32 [B,K], ids int32 [B,K])."""
@@ -128,7 +162,7 @@ def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
                      time[0], time[1], E.data_ptr(), M, k, _dtype_code(E),
                      0 if w is None else w.data_ptr(), item_row_begin, item_count,
                      global_item_base, K, top_s.data_ptr(), top_i.data_ptr(),
-                     ws.data_ptr(), ws.numel(), _stream(dev))
+                     ws.data_ptr(), ws.numel(), _status_ptr(status), _stream(dev))
     return top_s, top_i
 
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HHFM_ABI_VERSION 1
+#define HHFM_ABI_VERSION 2
 
 enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 
@@ -61,16 +61,23 @@ int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                        int32_t dtype, const float* w, float w0, float* out,
                        void* stream);
 
-/* Same, with tuning flags:
+/* Same, with tuning flags and an optional id status word:
  *   HHFM_FLAG_STREAM_TABLE — read embedding rows / ids and write `out` with
  *   non-temporal accesses, so the small, re-read bias table w stays resident
- *   in L2 / the 256 MB Infinity Cache while the (huge) table streams past. */
+ *   in L2 / the 256 MB Infinity Cache while the (huge) table streams past.
+ *   Bits 4..7 select measurement variants of the `w` gather's cache policy
+ *   (F=5, k=64 fp32 only; scripts/k1_wpolicy.py).
+ * status: NULL, or a device int32 the kernel ORs HHFM_STATUS_BAD_ID into when
+ *   it meets an id outside [0, features_M) (such ids are read as row 0 so the
+ *   kernel cannot fault).  hhfm_status_read() turns it into HHFM_EINVAL —
+ *   the InvalidArgumentError tf.nn.embedding_lookup raises (FM.py:99). */
 #define HHFM_FLAG_STREAM_TABLE 1
 #define HHFM_FM_ROWS_DEFAULT_FLAGS 0
+#define HHFM_STATUS_BAD_ID 1
 int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
                           const void* E, int64_t features_M, int32_t k,
                           int32_t dtype, const float* w, float w0, float* out,
-                          int32_t flags, void* stream);
+                          int32_t flags, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * H1 — HHFM per-row score (replaces `OUR.PositiveFeadback`,
@@ -86,6 +93,14 @@ int hhfm_hybrid_score_rows(const int32_t* idx, int64_t B, int32_t ncols,
                            int32_t time_begin, int32_t time_end,
                            const void* E, int64_t features_M, int32_t k,
                            int32_t dtype, float* out, void* stream);
+/* Same, with the optional id status word of hhfm_fm_score_rows_ex. */
+int hhfm_hybrid_score_rows_ex(const int32_t* idx, int64_t B, int32_t ncols,
+                              int32_t user_col, int32_t item_col,
+                              int32_t ctx_begin, int32_t ctx_end,
+                              int32_t time_begin, int32_t time_end,
+                              const void* E, int64_t features_M, int32_t k,
+                              int32_t dtype, float* out, int32_t* status,
+                              void* stream);
 
 /* ------------------------------------------------------------------------
  * M2/H2 — full-catalog score + fused top-K (replaces FM.topk, FM.py:172-198,
@@ -118,6 +133,16 @@ int hhfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t ncols,
                       int32_t item_count, int32_t global_item_base, int32_t K,
                       float* top_score, int32_t* top_idx, void* workspace,
                       size_t ws_bytes, void* stream);
+/* Same, with the optional id status word (query ids are checked on the
+ * stream before scoring; the item range is checked on the host). */
+int hhfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t ncols,
+                         int32_t mode, int32_t user_col, int32_t ctx_begin,
+                         int32_t ctx_end, int32_t time_begin, int32_t time_end,
+                         const void* E, int64_t features_M, int32_t k,
+                         int32_t dtype, const float* w, int32_t item_row_begin,
+                         int32_t item_count, int32_t global_item_base, int32_t K,
+                         float* top_score, int32_t* top_idx, void* workspace,
+                         size_t ws_bytes, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Top-K merge of R sorted partial lists per query (the item-sharded
@@ -320,6 +345,31 @@ int hhfm_libfm_encode(const char* buf, int64_t len, int32_t ncols, int64_t max_r
                       int64_t* distinct);
 int hhfm_loader_split(const int64_t* data, int64_t rows, int32_t ncols, int32_t item_col,
                       int64_t test_size, uint8_t* is_test);
+
+/* ------------------------------------------------------------------------
+ * Id validation (tf.nn.embedding_lookup raises InvalidArgumentError on an id
+ * outside [0, features_M): FM.py:99, OurModel7.py:105, AFM.py:104, DFM.py:105).
+ * Every kernel reads such an id as row 0 so it can never fault; callers that
+ * want TF's error pass a device status word:
+ *   hhfm_check_ids   — async: ORs HHFM_STATUS_BAD_ID into *status (device
+ *                      int32) if any of idx[0..n) is outside [0, features_M);
+ *                      covers every entry point without an _ex status form
+ *                      (AFM, DeepFM, training, harness).
+ *   hhfm_status_read — synchronises `stream`, reads and clears *status;
+ *                      returns HHFM_EINVAL if a bad id was seen, else HHFM_OK.
+ * ---------------------------------------------------------------------- */
+int hhfm_check_ids(const int32_t* idx, int64_t n, int64_t features_M, int32_t* status,
+                   void* stream);
+int hhfm_status_read(int32_t* status, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Measurement probe (not a scoring entry point): streams `bytes` (a multiple
+ * of 16, 16-B aligned) of device memory once with 16-B loads, so bench.py
+ * can report K1's HBM fraction against the box's measured read ceiling as
+ * well as the 8 TB/s spec.  `sink`: one device float (written only on an
+ * impossible data value, so the loads cannot be elided).
+ * ---------------------------------------------------------------------- */
+int hhfm_probe_stream_read(const void* buf, int64_t bytes, float* sink, void* stream);
 
 #ifdef __cplusplus
 }

@@ -26,16 +26,17 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     lib.hhfm_abi_version.restype = ctypes.c_int
-    assert lib.hhfm_abi_version() == 1
+    assert lib.hhfm_abi_version() == 2
 
 
 def test_pybind_module_binds_the_abi():
     from hhfm_amd._native import native
     m = native()
     for n in ["fm_score_rows", "hybrid_score_rows", "catalog_topk", "catalog_topk_workspace",
-              "topk_merge", "topk_merge_host"]:
+              "topk_merge", "topk_merge_host", "check_ids", "status_read",
+              "probe_stream_read"]:
         assert hasattr(m, n)
-    assert m.abi_version() == 1
+    assert m.abi_version() == 2
 
 
 def test_argument_validation_without_device():
@@ -59,10 +60,10 @@ def test_catalog_argument_errors_raise_valueerror():
         m.catalog_topk_workspace(10, 100, 64, 65)     # K > 64
     with pytest.raises(ValueError):                  # K > item_count
         m.catalog_topk(1, 10, 5, 1, 0, 2, 5, 0, 0, 1, 1000, 64, 0, 0, 900, 10, 0, 20,
-                       1, 1, 1, 1 << 20, 0)
+                       1, 1, 1, 1 << 20, 0, 0)
     with pytest.raises(ValueError):                  # k not a multiple of 8 (fp32)
         m.catalog_topk(1, 10, 5, 1, 0, 2, 5, 0, 0, 16, 1000, 20, 0, 0, 900, 100, 0, 20,
-                       1, 1, 1, 1 << 20, 0)
+                       1, 1, 1, 1 << 20, 0, 0)
     assert m.catalog_topk_workspace(300, 4082, 64, 20) > 300 * 64 * 4
 
 
@@ -80,3 +81,80 @@ def test_host_merge_matches_sort():
         cand = sorted(zip((-sc[:, b]).ravel().tolist(), ids[:, b].ravel().tolist()))[:K]
         assert [c[1] for c in cand] == i[b].tolist()
         assert [-c[0] for c in cand] == s[b].tolist()
+
+
+def test_status_abi_argument_errors_without_device():
+    lib = ctypes.CDLL(LIB)
+    lib.hhfm_check_ids.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.c_void_p, ctypes.c_void_p]
+    lib.hhfm_status_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.hhfm_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_void_p]
+    assert lib.hhfm_check_ids(None, 10, 5, None, None) == -1       # no status word
+    assert lib.hhfm_status_read(None, None) == -1
+    assert lib.hhfm_probe_stream_read(None, 64, None, None) == -1
+
+
+@pytest.mark.gpu
+def test_bad_ids_reach_c_callers_as_einval():
+    """A C caller of the ABI gets HHFM_EINVAL (tf.nn.embedding_lookup's
+    InvalidArgumentError, FM.py:99) for an out-of-range id through the status
+    word: in-kernel for K1 / H1, checked on the stream for the catalog."""
+    lib = ctypes.CDLL(LIB)
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
+    lib.hhfm_fm_score_rows_ex.argtypes = [vp, i64, i32, vp, i64, i32, i32, vp, ctypes.c_float,
+                                          vp, i32, vp, vp]
+    lib.hhfm_hybrid_score_rows_ex.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp,
+                                              i64, i32, i32, vp, vp, vp]
+    lib.hhfm_status_read.argtypes = [vp, vp]
+    M, k = 1000, 64
+    E = torch.randn(M, k, device="cuda") * 0.01
+    w = torch.zeros(M, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    out = torch.empty(4097, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    good = torch.randint(0, M, (4097, 5), dtype=torch.int32, device="cuda")
+    for bad_value in (M, -1, 2**31 - 1):
+        for kk in (64, 20):                            # fast and generic kernels
+            Ek = E[:, :kk].contiguous()
+            X = good.clone()
+            X[4000, 3] = bad_value
+            for fn in ("fm", "hybrid"):
+                if fn == "fm":
+                    rc = lib.hhfm_fm_score_rows_ex(X.data_ptr(), 4097, 5, Ek.data_ptr(), M, kk, 0,
+                                                   w.data_ptr(), 0.0, out.data_ptr(), 0,
+                                                   st.data_ptr(), stream)
+                else:
+                    rc = lib.hhfm_hybrid_score_rows_ex(X.data_ptr(), 4097, 5, 0, 1, 2, 5, 0, 0,
+                                                       Ek.data_ptr(), M, kk, 0, out.data_ptr(),
+                                                       st.data_ptr(), stream)
+                assert rc == 0
+                assert lib.hhfm_status_read(st.data_ptr(), stream) == -1, (bad_value, kk, fn)
+                # the word is cleared by the read; a clean batch reports OK
+                lib.hhfm_fm_score_rows_ex(good.data_ptr(), 4097, 5, Ek.data_ptr(), M, kk, 0,
+                                          w.data_ptr(), 0.0, out.data_ptr(), 0, st.data_ptr(),
+                                          stream)
+                assert lib.hhfm_status_read(st.data_ptr(), stream) == 0
+    # catalog: a bad context id in a query row
+    from hhfm_amd import ops
+    q = good[:50].clone()
+    q[7, 2] = M + 3
+    ops.catalog_topk(q, E, ops.MODE_HHFM, 20, 100, 500, 0, None, 0, (2, 5), (0, 0), status=st)
+    assert lib.hhfm_status_read(st.data_ptr(), stream) == -1
+    q[7, 2] = 5
+    q[9, 1] = -7                                       # item column: not read by the score
+    ops.catalog_topk(q, E, ops.MODE_HHFM, 20, 100, 500, 0, None, 0, (2, 5), (0, 0), status=st)
+    assert lib.hhfm_status_read(st.data_ptr(), stream) == 0
+
+
+@pytest.mark.gpu
+def test_wide_ids_are_checked_before_narrowing():
+    """2**32 + 5 must raise, not wrap to 5 (_idx narrowing)."""
+    from hhfm_amd.FM import FM
+    m = FM(5, 100, 10, 50, 16, 0.1, 0.1, 1, "AdagradOptimizer", 0, 0)
+    X = np.array([[0, 10, 60, 61, 2**32 + 5]], dtype=np.int64)
+    with pytest.raises(ValueError):
+        m.score_rows(X)
+    with pytest.raises(ValueError):
+        m.score_rows(torch.from_numpy(X))
+    assert m.score_rows(np.array([[0, 10, 60, 61, 5]], dtype=np.int64)).shape == (1, 1)

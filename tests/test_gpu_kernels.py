@@ -76,7 +76,7 @@ def test_fm_score_rows_flag_variants_bit_identical(dtype, k, F):
         o = torch.full((B,), float("nan"), device="cuda")
         native().fm_score_rows_ex(X.data_ptr(), B, F, E.data_ptr(), M, k,
                                   1 if dtype == "bf16" else 0, w.data_ptr(), 0.003,
-                                  o.data_ptr(), flags, st)
+                                  o.data_ptr(), flags, 0, st)
         outs.append(o.cpu())
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
