@@ -445,24 +445,28 @@ def c5_leg(dev, world, rank, rows, reps=3):
 
 
 def stream_read_peak(buf, reps=5):
-    """The box's measured HBM read ceiling: hhfm_probe_stream_read (one
-    16-B-per-lane sequential pass) over `buf`, best of `reps`, GB/s."""
+    """The box's measured HBM read ceiling: hhfm_probe_stream_read over
+    `buf` (grid-stride, contiguous-chunk and non-temporal chunk variants),
+    best launch of `reps` per variant, GB/s -> (best, {variant: GB/s})."""
     from hhfm_amd._native import native
     dev = buf.device
     sink = torch.zeros(1, device=dev)
     nbytes = (buf.numel() * buf.element_size()) & ~15
     st = torch.cuda.current_stream(dev).cuda_stream
-    native().probe_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), st)
-    best = None
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        native().probe_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), st)
-        e1.record()
-        e1.synchronize()
-        ms = e0.elapsed_time(e1)
-        best = ms if best is None else min(best, ms)
-    return nbytes / (best * 1e-3) / 1e9
+    rates = {}
+    for mode, name in ((0, "grid_stride"), (1, "chunked"), (2, "chunked_nt")):
+        native().probe_stream_read(buf.data_ptr(), nbytes, mode, sink.data_ptr(), st)
+        best = None
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            native().probe_stream_read(buf.data_ptr(), nbytes, mode, sink.data_ptr(), st)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        rates[name] = nbytes / (best * 1e-3) / 1e9
+    return max(rates.values()), rates
 
 
 def main():
@@ -527,7 +531,7 @@ def main():
     # that cross HBM at that granularity are 2 rows x 256 B + 2 w lines x 128 B
     # + ids + out = 792 B/row at k=64.
     bpr_lines = 2 * args.k * 4 + 2 * 128 + 5 * 4 + 4
-    peak_meas = stream_read_peak(E)
+    peak_meas, peak_variants = stream_read_peak(E)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -561,8 +565,9 @@ def main():
                      "survey_bytes_per_row": bpr_survey,
                      "survey_rate_GBps": bpr_survey * args.rows / (kern_ms * 1e-3) / 1e9,
                      "peak_measured": peak_meas,
-                     "peak_measured_how": "hhfm_probe_stream_read: one sequential 16-B/lane "
-                                          "read of the 4.3 GB table, best of 5, this box",
+                     "peak_measured_how": "hhfm_probe_stream_read: one 16-B/lane read of the "
+                                          "4.3 GB table, best variant and launch of 5, this box",
+                     "peak_measured_variants": peak_variants,
                      "frac_vs_measured": (achieved / peak_meas) if peak_meas else None,
                      "line_bytes_per_row": bpr_lines,
                      "line_rate_GBps": bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9,

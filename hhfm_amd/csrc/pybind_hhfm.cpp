@@ -130,11 +130,12 @@ PYBIND11_MODULE(_hhfm, m) {
     return rc;
   });
 
-  m.def("probe_stream_read", [](uptr buf, int64_t bytes, uptr sink, uptr stream) {
+  m.def("probe_stream_read", [](uptr buf, int64_t bytes, int mode, uptr sink, uptr stream) {
     int rc;
     {
       py::gil_scoped_release nogil;
-      rc = hhfm_probe_stream_read(P<const void>(buf), bytes, P<float>(sink), P<void>(stream));
+      rc = hhfm_probe_stream_read(P<const void>(buf), bytes, mode, P<float>(sink),
+                                  P<void>(stream));
     }
     check(rc, "hhfm_probe_stream_read");
   });

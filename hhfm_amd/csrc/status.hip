@@ -51,6 +51,7 @@ int launch_check_query_ids(const int32_t* q, int64_t B, int ncols, int ucol, int
   return (int)hipGetLastError();
 }
 
+// mode 0: grid-stride (each wave 1 KiB, consecutive waves adjacent)
 __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4_t* __restrict__ p,
                                                           int64_t n16, float* sink) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -61,6 +62,27 @@ __global__ __launch_bounds__(256) void stream_read_kernel(const u32x4_t* __restr
     acc ^= a ^ b ^ c ^ d;
   }
   for (; i < n16; i += stride) acc ^= p[i];
+  if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9e3779b9u) sink[0] = 1.f;
+}
+
+// modes 1/2: each workgroup streams one contiguous chunk, 8 loads in flight
+// per lane; NT = non-temporal loads
+template <bool NT>
+__global__ __launch_bounds__(256) void stream_read_chunk_kernel(const u32x4_t* __restrict__ p,
+                                                                int64_t n16, int64_t chunk,
+                                                                float* sink) {
+  const int64_t b0 = (int64_t)blockIdx.x * chunk;
+  const int64_t b1 = b0 + chunk < n16 ? b0 + chunk : n16;
+  u32x4_t acc = {0u, 0u, 0u, 0u};
+  int64_t i = b0 + threadIdx.x;
+  for (; i + 7 * 256 < b1; i += 8 * 256) {
+    u32x4_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = load16<NT>(p + i + j * 256);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j];
+  }
+  for (; i < b1; i += 256) acc ^= load16<NT>(p + i);
   if ((acc[0] ^ acc[1] ^ acc[2] ^ acc[3]) == 0x9e3779b9u) sink[0] = 1.f;
 }
 
@@ -89,16 +111,30 @@ extern "C" int hhfm_status_read(int32_t* status, void* stream) {
   return (h & HHFM_STATUS_BAD_ID) ? HHFM_EINVAL : HHFM_OK;
 }
 
-extern "C" int hhfm_probe_stream_read(const void* buf, int64_t bytes, float* sink,
-                                      void* stream) {
-  if (!buf || !sink || bytes < 16 || (bytes & 15) ||
+extern "C" int hhfm_probe_stream_read(const void* buf, int64_t bytes, int32_t mode,
+                                      float* sink, void* stream) {
+  if (!buf || !sink || bytes < 16 || (bytes & 15) || mode < 0 || mode > 2 ||
       (reinterpret_cast<uintptr_t>(buf) & 15))
     return HHFM_EINVAL;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipLaunchKernelGGL(stream_read_kernel, dim3(cus * 8), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream),
-                     reinterpret_cast<const u32x4_t*>(buf), bytes / 16, sink);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const u32x4_t* p = reinterpret_cast<const u32x4_t*>(buf);
+  const int64_t n16 = bytes / 16;
+  if (mode == 0) {
+    hipLaunchKernelGGL(stream_read_kernel, dim3(cus * 8), dim3(256), 0, s, p, n16, sink);
+  } else {
+    const int64_t grid = (int64_t)cus * 8;
+    const int64_t step = 8 * 256;
+    const int64_t chunk = ((n16 + grid - 1) / grid + step - 1) / step * step;
+    const int64_t nb = (n16 + chunk - 1) / chunk;
+    if (mode == 1)
+      hipLaunchKernelGGL(stream_read_chunk_kernel<false>, dim3((int)nb), dim3(256), 0, s, p,
+                         n16, chunk, sink);
+    else
+      hipLaunchKernelGGL(stream_read_chunk_kernel<true>, dim3((int)nb), dim3(256), 0, s, p,
+                         n16, chunk, sink);
+  }
   return (int)hipGetLastError();
 }

@@ -366,10 +366,13 @@ int hhfm_status_read(int32_t* status, void* stream);
  * Measurement probe (not a scoring entry point): streams `bytes` (a multiple
  * of 16, 16-B aligned) of device memory once with 16-B loads, so bench.py
  * can report K1's HBM fraction against the box's measured read ceiling as
- * well as the 8 TB/s spec.  `sink`: one device float (written only on an
- * impossible data value, so the loads cannot be elided).
+ * well as the 8 TB/s spec.  mode 0: grid-stride; 1: one contiguous chunk per
+ * workgroup, 8 loads in flight per lane; 2: as 1 with non-temporal loads.
+ * `sink`: one device float (written only on an impossible data value, so the
+ * loads cannot be elided).
  * ---------------------------------------------------------------------- */
-int hhfm_probe_stream_read(const void* buf, int64_t bytes, float* sink, void* stream);
+int hhfm_probe_stream_read(const void* buf, int64_t bytes, int32_t mode, float* sink,
+                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ Frappe README forbids redistribution):
   synth_frappe.libfm / synth_jiaju.libfm   synthetic libfm inputs
   loaddata_*.npz        LoadData outputs for np.random.seed(2016)
   fm.npz hhfm_*.npz afm.npz dfm.npz        model-graph outputs (out / topk)
+  losses.npz            each model's `self.loss` at seeded weights + batch
   harness.npz + harness.json               sample_negative / evaluate_TopK /
                                            evaluate_AUC outputs
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
@@ -216,6 +217,87 @@ def gen_dfm():
 
 
 # ---------------------------------------------------------------------------
+# training objectives: each reference model's own `self.loss` graph
+# (FM.py:123-126, OurModel7.py:172-184, AFM.py:144-148, DFM.py:139-152)
+# evaluated at seeded weights on a seeded batch with negatives
+# ---------------------------------------------------------------------------
+def gen_losses():
+    out = {}
+    nu, ni, ctx = 40, 150, (7, 2, 3)
+    M = vocab(nu, ni, ctx)
+
+    # FM: MSE on positives (label 1) + sampled negatives (label 0, FM.py:248)
+    rng = np.random.default_rng(701)
+    k = 16
+    m = RFM.FM(5, M, nu, ni, k, 0.1, 0.1, 1, "AdagradOptimizer", 0, 0)
+    E = rng.normal(0, 0.01, (M, k)).astype(np.float32)
+    w = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    m.weights["feature_embeddings"].value = E
+    m.weights["feature_bias"].value = w
+    m.weights["bias"].value = np.float32(0.03)
+    X = rows(rng, 96, nu, ni, ctx)
+    Y = np.concatenate([np.ones(48), np.zeros(48)]).reshape(-1, 1).astype(np.float32)
+    loss = m.sess.run(m.loss, feed_dict={m.train_features: X, m.train_labels: Y,
+                                         m.dropout_keep: 1.0, m.train_phase: True})
+    out.update(fm_E=E, fm_w=w[:, 0], fm_w0=np.float32(0.03), fm_X=X, fm_Y=Y[:, 0],
+               fm_lamda=np.float32(0.1), fm_loss=np.float32(loss))
+
+    # HHFM (frappe layout): −Σ log σ(s⁺ − max_neg s⁻) + λ‖E‖²/2
+    rng = np.random.default_rng(702)
+    m = RM7.OUR(3, 0, M, nu, ni, k, 0.1, 0.01, "AdagradOptimizer", True, False)
+    E = rng.normal(0, 0.3, (M, k)).astype(np.float32)   # wide: the sigmoid is not saturated at 0.5
+    m.weights["feature_embeddings"].value = E
+    X = rows(rng, 80, nu, ni, ctx)
+    Neg = rng.integers(nu, nu + ni, (80, 10)).astype(np.int32)
+    Neg[3, 4] = Neg[3, 7]                                   # a tie in reduce_max
+    loss = m.sess.run(m.loss, feed_dict={m.Pos: X[:, :2], m.Fea: X[:, 2:], m.Neg: Neg})
+    out.update(hhfm_E=E, hhfm_X=X, hhfm_Neg=Neg, hhfm_lamda=np.float32(0.01),
+               hhfm_loss=np.float32(loss))
+
+    # AFM: MSE with labels {1, -1} (AFM.py:317) + λ‖attention_W‖²/2
+    rng = np.random.default_rng(703)
+    np.random.seed(703)
+    ka = 16
+    m = RAFM.AFM(nu, ni, M, 1, [ka, ka], None, 0.1, 2.0, [1, 1], "AdagradOptimizer", 0.999, 5)
+    E = rng.normal(0, 0.1, (M, ka)).astype(np.float32)
+    w = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
+    m.weights["feature_embeddings"].value = E
+    m.weights["feature_bias"].value = w
+    m.weights["bias"].value = np.float32(0.02)
+    X = rows(rng, 64, nu, ni, ctx)
+    Y = np.concatenate([np.ones(32), -np.ones(32)]).reshape(-1, 1).astype(np.float32)
+    loss = m.sess.run(m.loss, feed_dict={m.train_features: X, m.train_labels: Y,
+                                         m.dropout_keep: [1.0, 1.0], m.train_phase: True})
+    W = m.weights
+    out.update(afm_E=E, afm_w=w[:, 0], afm_w0=np.float32(0.02), afm_X=X, afm_Y=Y[:, 0],
+               afm_lamda=np.float32(2.0), afm_attention_W=W["attention_W"].value,
+               afm_attention_b=W["attention_b"].value, afm_attention_p=W["attention_p"].value,
+               afm_prediction=W["prediction"].value, afm_loss=np.float32(loss))
+
+    # DeepFM: MSE with labels {1, -1} (DFM.py:286) + l2_reg on projection + layers
+    rng = np.random.default_rng(704)
+    np.random.seed(704)
+    m = RDFM.DeepFM(nu, ni, M, 5, k, [32, 24], tf1_numpy.nn.relu, 0.01, 0, 0.05)
+    E = rng.normal(0, 0.05, (M, k)).astype(np.float32)
+    w = rng.uniform(0, 1, (M, 1)).astype(np.float32)
+    m.weights["feature_embeddings"].value = E
+    m.weights["feature_bias"].value = w
+    X = rows(rng, 64, nu, ni, ctx)
+    Y = np.concatenate([np.ones(32), -np.ones(32)]).reshape(-1, 1).astype(np.float32)
+    loss = m.sess.run(m.loss, feed_dict={m.feat_index: X, m.label: Y})
+    W = m.weights
+    out.update(dfm_E=E, dfm_w=w[:, 0], dfm_X=X, dfm_Y=Y[:, 0], dfm_l2=np.float32(0.05),
+               dfm_concat_projection=W["concat_projection"].value,
+               dfm_concat_bias=np.float32(W["concat_bias"].value),
+               **{f"dfm_layer_{i}": W[f"layer_{i}"].value for i in range(2)},
+               **{f"dfm_bias_{i}": W[f"bias_{i}"].value for i in range(2)},
+               dfm_loss=np.float32(loss))
+    out.update(n_user=nu, n_item=ni)
+    save("losses.npz", **out)
+    print("losses", {kk: float(v) for kk, v in out.items() if kk.endswith("_loss")})
+
+
+# ---------------------------------------------------------------------------
 # harness (Train.* methods, unmodified, with a stand-in model)
 # ---------------------------------------------------------------------------
 class _OracleModel:
@@ -348,6 +430,7 @@ def main():
     gen_hhfm("resturant", 200, 600, (5, 4, 6, 3, 7), 5, 16, 203)
     gen_afm()
     gen_dfm()
+    gen_losses()
     gen_harness(d)
     gen_frappe_real()
 

@@ -88,11 +88,11 @@ def test_status_abi_argument_errors_without_device():
     lib.hhfm_check_ids.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                    ctypes.c_void_p, ctypes.c_void_p]
     lib.hhfm_status_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    lib.hhfm_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                           ctypes.c_void_p]
+    lib.hhfm_probe_stream_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
     assert lib.hhfm_check_ids(None, 10, 5, None, None) == -1       # no status word
     assert lib.hhfm_status_read(None, None) == -1
-    assert lib.hhfm_probe_stream_read(None, 64, None, None) == -1
+    assert lib.hhfm_probe_stream_read(None, 64, 0, None, None) == -1
 
 
 @pytest.mark.gpu

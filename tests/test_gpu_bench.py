@@ -54,7 +54,7 @@ def test_c4_shards_merge_to_the_unsharded_top20():
 def test_stream_read_probe_and_c5_leg_run():
     dev = torch.device("cuda", 0)
     buf = torch.empty(1 << 28, dtype=torch.uint8, device=dev)
-    gbs = bench.stream_read_peak(buf, reps=3)
-    assert 500 < gbs < 20000, gbs
+    gbs, var = bench.stream_read_peak(buf, reps=3)
+    assert 500 < gbs < 20000 and len(var) == 3, (gbs, var)
     r = bench.c5_leg(dev, 1, 0, 100_000, reps=1)
     assert np.isfinite(r["rows_per_s"]) and r["roofline"]["frac"] > 0
