@@ -309,9 +309,11 @@ __global__ __launch_bounds__(256) void catalog_main(
     if (HHFM_MAIN_PRIO) __builtin_amdgcn_s_setprio(0);
     if constexpr (FM) {
       // D[i][j] += w_i * 1 + 1 * (q_j·f_j)   (bias row/col folded into one MFMA)
-      if constexpr (STORE)   // D[q][i] += (q_q·f_q) * 1 + 1 * w_i
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? cq : 1.f,
-                                                   h == 0 ? 1.f : wcur, acc, 0, 0, 0);
+      // STORE: D[q][i] += 1 * w_i + (q_q·f_q) * 1 — the same products at the
+      // same k positions as the selecting kernel, so both give the same bits
+      if constexpr (STORE)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? 1.f : cq,
+                                                   h == 0 ? wcur : 1.f, acc, 0, 0, 0);
       else
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f,
                                                    h == 0 ? 1.f : cq, acc, 0, 0, 0);
@@ -608,7 +610,9 @@ struct Plan {
   int Ss, ips;           //   its item splits and items per split
   bool dense;            // small catalog, other k: score matrix + dense top-K
   int64_t ldsc;
-  size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, total;
+  int seed_n;            // streaming path: items of the threshold seed (0 = none)
+  size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
+      off_seed_i, total;
 };
 
 // Small catalogs (evaluate_TopK over Frappe's 4,082 items is the case): the
@@ -626,6 +630,22 @@ static bool small_catalog(int64_t B, int32_t N, int32_t k) {
   const char* e = getenv("HHFM_CATALOG_SMALL");
   if (!e || e[0] != '1') return false;   // opt-in: C3 0.12 ms vs 0.096 ms on the dense path
   return dense_catalog(B, N) && (k == 32 || k == 64 || k == 128);
+}
+
+// Threshold seed of the streaming path (default on; HHFM_CATALOG_SEED=0 off):
+// the exact top-K of the first seed_n items (STORE score matrix + dense
+// top-K) gives every query a K-th score t before the main pass.  K catalog
+// items score >= t, so the global K-th is >= t and items below t can be
+// dropped; without it every item split warms its lists up from -inf and the
+// per-split thresholds (and their atomicMax hint, a max of per-split K-ths)
+// stay near the K-th of one split, which costs ~K·ln(items per split / K)
+// list insertions per query and split.  The STORE kernel computes every
+// score with the same MFMA products in the same k order as the selecting
+// kernel (operands swapped: D = Aᵀ-layout), so t is bit-exactly a score the
+// main pass reproduces (tests/test_gpu_kernels.py: seeded == unseeded).
+static bool catalog_seed() {
+  const char* e = getenv("HHFM_CATALOG_SEED");
+  return !(e && e[0] == '0');
 }
 
 static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
@@ -668,6 +688,24 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
   if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
+  // seed: up to 32,768 items and a 128 MiB score matrix, only when the
+  // catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
+  p.seed_n = 0;
+  if (!p.small && !p.dense && catalog_seed()) {
+    int64_t sn = ((int64_t)32 << 20) / p.Bpad;
+    sn = (sn > 32768 ? 32768 : sn) & ~int64_t(31);
+    if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
+  }
+  p.off_seed_sc = off;
+  if (p.seed_n) {
+    off += align256((size_t)B * p.seed_n * sizeof(float));
+    p.off_seed_s = off;
+    off += align256((size_t)B * K * sizeof(float));
+    p.off_seed_i = off;
+    off += align256((size_t)B * K * sizeof(int32_t));
+  } else {
+    p.off_seed_s = p.off_seed_i = off;
+  }
   p.total = off;
   return p;
 }
@@ -754,6 +792,14 @@ static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H
     default: return false;
   }
   return true;
+}
+
+// gthr[b] = key of query b's K-th seed score (the seed's lists are sorted)
+__global__ __launch_bounds__(256) void seed_thr_kernel(const float* __restrict__ seed_s,
+                                                       int64_t B, int K,
+                                                       int32_t* __restrict__ gthr) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) gthr[b] = fkey(seed_s[b * K + (K - 1)]);
 }
 
 static void launch_merge(const float* in_s, const int32_t* in_i, int R, int64_t B,
@@ -934,6 +980,21 @@ extern "C" int hhfm_catalog_topk_ex(
   const int32_t gbase = global_item_base;  // order-preserving shift
   const bool fm = mode == HHFM_MODE_FM;
   bool ok;
+  if (p.seed_n) {   // threshold seed (catalog_seed above)
+    float* ssc = reinterpret_cast<float*>(ws + p.off_seed_sc);
+    float* sds = reinterpret_cast<float*>(ws + p.off_seed_s);
+    int32_t* sdi = reinterpret_cast<int32_t*>(ws + p.off_seed_i);
+    const float* wv = (fm && w) ? w : nullptr;
+    const int64_t irb = item_row_begin;
+    if (bf16) ok = fm ? dispatch_store<true, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st)
+                      : dispatch_store<true, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st);
+    else ok = fm ? dispatch_store<false, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st)
+                 : dispatch_store<false, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st);
+    if (!ok) return HHFM_EUNSUPPORTED;
+    launch_topk_dense(ssc, B, p.seed_n, p.seed_n, K, 0, sds, sdi, st);
+    hipLaunchKernelGGL(seed_thr_kernel, dim3((int)((B + 255) / 256)), dim3(256), 0, st, sds, B,
+                       K, gthr);
+  }
 #define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, st
   if (K <= 32) {
     if (bf16) ok = fm ? dispatch_kt<true, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<true, 32, false>(HHFM_MAIN_ARGS);

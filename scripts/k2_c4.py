@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""K2 at the C4 per-GPU shape (HHFM k=128, 1,024 queries x 1.25M-item shard,
+top-20): median kernel time per variant (HIP events), fp32 and bf16 tables.
+Variants are environment switches read per call (HHFM_CATALOG_SEED,
+HHFM_CATALOG_EXACT).  usage: python scripts/k2_c4.py [--reps N]"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from hhfm_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--items", type=int, default=1_250_000)
+    ap.add_argument("--variants", default="seed,noseed")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    nu, N, k, B, K = 1 << 20, a.items, 128, 1024, 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(3)
+    E32 = torch.empty(nu + 12 + N, k, device=dev).normal_(0, 0.01, generator=g)
+    A = torch.stack([torch.randint(0, nu, (B,), generator=g, device=dev),
+                     torch.zeros(B, dtype=torch.int64, device=dev),
+                     nu + torch.randint(0, 7, (B,), generator=g, device=dev),
+                     nu + 7 + torch.randint(0, 2, (B,), generator=g, device=dev),
+                     nu + 9 + torch.randint(0, 3, (B,), generator=g, device=dev)],
+                    1).to(torch.int32).contiguous()
+    res = {}
+    for tname, E in (("fp32", E32), ("bf16", E32.to(torch.bfloat16))):
+        ref = None
+        for var in a.variants.split(","):
+            os.environ["HHFM_CATALOG_SEED"] = "0" if "noseed" in var else "1"
+            os.environ["HHFM_CATALOG_EXACT"] = "1" if "exact" in var else "0"
+
+            def run():
+                return ops.catalog_topk(A, E, ops.MODE_HHFM, K, nu + 12, N, 0, None, 0,
+                                        (2, 5), (0, 0))
+            run()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                s, i = run()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            same = None
+            if ref is None:
+                ref = (s.clone(), i.clone())
+            else:
+                same = bool(torch.equal(i, ref[1]))
+            ms = float(np.median(ts))
+            res[f"{tname}_{var}"] = {"ms": ms, "TFLOPs": 2.0 * k * B * N / (ms * 1e-3) / 1e12,
+                                     "ids_equal_first_variant": same}
+            print(json.dumps({f"{tname}_{var}": res[f"{tname}_{var}"]}), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
