@@ -23,6 +23,8 @@
 // Order everywhere: score descending, item index ascending (tf.nn.top_k).
 #include "gemm_mfma.h"
 
+#include <algorithm>
+
 namespace hhfm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -38,6 +40,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #endif
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
+#endif
+#ifndef HHFM_RING_SLOTS
+#define HHFM_RING_SLOTS 4   // catalog_ring bf16 tile slots (R-1 tiles of DMA lead)
 #endif
 #ifndef HHFM_MAIN_PF
 #define HHFM_MAIN_PF 1   // item tiles in flight per wave (1 or 2)
@@ -452,6 +457,320 @@ __global__ __launch_bounds__(256) void catalog_main(
 }
 
 // ---------------------------------------------------------------------------
+// 2a'. catalog_ring — the streaming kernel with the item tiles staged in LDS
+//
+// catalog_main streams every item tile into each wave's registers one tile
+// ahead: at the C4 shape that leaves the SIMDs parked on memory half the time
+// (bf16 tables: SQ_WAIT_ANY 50 % of wave cycles, MFMA busy 35 %) and, for
+// fp32 tables, every wave splits the same tile into its three bf16 pieces (4
+// copies of ~320 VALU per tile).  Here a workgroup is 4 waves = 128 queries x
+// one item split (two workgroups per CU, two waves per SIMD), and the tile is
+// fetched ONCE per workgroup:
+//   * bf16 tables: a ring of R tile slots, filled R-1 tiles ahead by LDS-DMA
+//     (global_load_lds_dwordx4) with per-lane source addresses chosen so the
+//     image is [k16 step][half][item] x 16 B — every A-operand ds_read_b128
+//     reads 16 consecutive 16-B slots (conflict-free);
+//   * fp32 tables: each lane loads NU/4 (item, 16-k step, half) units of the
+//     tile two tiles ahead into registers, splits them into their three bf16
+//     pieces (exact, split3x8) and stores them into a double-buffered piece
+//     image [piece][step][half][item]: 1/256 of the split work per lane.
+// One s_barrier per tile (4 waves; the other workgroup on the CU is not
+// coupled to it).  The MFMA products, their k order and the selection are
+// catalog_main's (SPLIT path), so scores are bit-identical to it and to the
+// STORE seed.  Candidates are inserted one by one (the dense sort + merge
+// path and its LDS transpose buffer are dropped): the kernel runs only behind
+// the threshold seed, which leaves a few insertions per query and split.
+// Used for K <= 32, bf16 k = 128 and fp32 k in {64, 128}.
+// ---------------------------------------------------------------------------
+template <bool BF16, int KT, int NW>
+struct RingCfg {
+  static constexpr int kRingWaves = NW;                      // waves (x 32 queries) per workgroup
+  static constexpr int kRowB = KT * 32;                      // bytes per item row
+  static constexpr int kTileB = kTile * kRowB;               // one raw tile
+  static constexpr int kNU = BF16 ? KT : KT / 2;             // 16-k MFMA steps per tile
+  static constexpr int kSlots = BF16 ? HHFM_RING_SLOTS : 2;
+  static constexpr int kStageB = BF16 ? kSlots * kTileB : 2 * 3 * kNU * 1024;
+  static constexpr int kListB = kRingWaves * kQPerWave * 32 * 8;   // KPAD 32
+  static constexpr int kSmem = kStageB + kListB;
+  static constexpr int kDma = BF16 ? KT / kRingWaves : 0;    // DMA instructions per wave and tile
+  static constexpr int kUnits = BF16 ? 0 : (kNU + NW - 1) / NW;   // fp32 split units per lane
+};
+
+template <bool BF16, int KT, bool FM, int NW>
+__global__ __launch_bounds__(NW * 64) void catalog_ring(
+    const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
+    const char* __restrict__ E, int64_t item_row_begin, int32_t N,
+    const float* __restrict__ w, int K, int S, int tiles_per_split, int nqb,
+    float* __restrict__ out_s, int32_t* __restrict__ out_i, int64_t ostride_b,
+    int64_t ostride_s, int32_t gbase, int32_t* __restrict__ gthr) {
+  using Cfg = RingCfg<BF16, KT, NW>;
+  constexpr int kRingWaves = NW;
+  constexpr int kRingQ = NW * kQPerWave;
+  constexpr int KPAD = 32;
+  constexpr int k = BF16 ? KT * 16 : KT * 8;
+  constexpr int64_t ROWB = Cfg::kRowB;
+  constexpr int NU = Cfg::kNU;
+  constexpr int R = Cfg::kSlots;
+  static_assert(BF16 ? KT % kRingWaves == 0 : true, "ring kernel: bf16 k >= 16 * waves");
+
+  __shared__ __attribute__((aligned(16))) char smem[Cfg::kSmem];
+  char* stage = smem;
+  float* lst_s = reinterpret_cast<float*>(smem + Cfg::kStageB);
+  int32_t* lst_i = reinterpret_cast<int32_t*>(smem + Cfg::kStageB + Cfg::kListB / 2);
+
+  const int wid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wid / nqb;
+  const int g = wid - split * nqb;
+  const int wv = threadIdx.x / kWave;
+  const int l = lane_id();
+  const int j = l & 31;   // query column (MFMA B/C layout) / item row (A layout)
+  const int h = l >> 5;   // k half (A/B layout) / row half (C layout)
+  const int64_t q0 = (int64_t)g * kRingQ + wv * kQPerWave;
+  const bool wave_live = q0 < B;   // idle waves still take part in barriers and staging
+
+  const int ntiles = (N + kTile - 1) / kTile;
+  const int tb0 = split * tiles_per_split;
+  const int tb1 = min(tb0 + tiles_per_split, ntiles);
+  const int item_end = min(tb1 * kTile, N);
+
+  float* ls = lst_s + wv * (kQPerWave * KPAD);
+  int32_t* li = lst_i + wv * (kQPerWave * KPAD);
+  for (int x = l; x < kQPerWave * KPAD; x += kWave) {
+    ls[x] = kNegInf;
+    li[x] = kNoIdx;
+  }
+
+  // B operand: the wave's 32 queries split into three bf16 pieces (catalog_main)
+  const int64_t q = q0 + j;
+  constexpr int EPC = BF16 ? 8 : 4;
+  bf16x8 qp[3][NU];
+  {
+    const int64_t qs = q < B ? q : 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      float x[8];
+      if constexpr (BF16) {
+        const float4* src = reinterpret_cast<const float4*>(H + qs * k + (2 * u + h) * EPC);
+        const float4 a = src[0], b = src[1];
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      } else {   // chunks 2u and 2u+1 of the lane half: k {16u+4h..+3, 16u+8+4h..+3}
+        const float4 a = *reinterpret_cast<const float4*>(H + qs * k + (4 * u + h) * EPC);
+        const float4 b = *reinterpret_cast<const float4*>(H + qs * k + (4 * u + 2 + h) * EPC);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      }
+      split3x8(x, qp[0][u], qp[1][u], qp[2][u]);
+    }
+  }
+  float cq = 0.f;
+  if constexpr (FM) cq = q < B ? cst[q] : 0.f;
+  // the threshold seed (and any K-th an earlier split published): read once —
+  // behind the seed the per-split lists rarely beat it, so a per-tile reload
+  // of the hint would only put a global load on every tile's critical path
+  float thr = (q < B) ? fkey_inv(gthr[q]) : __builtin_huge_valf();
+
+  auto item_row = [&](int tile, int jj) -> const char* {
+    tile = tile < tb1 ? tile : tb1 - 1;
+    int item = tile * kTile + jj;
+    item = item < N ? item : N - 1;
+    return E + (item_row_begin + item) * ROWB;
+  };
+
+  // ---- staging ----
+  // bf16: DMA instruction d of wave wv moves LDS units [64(wv + 4d), +64):
+  // unit P = (t*2 + h)*32 + j  <-  item j, bytes [32t + 16h, +16) of its row
+  auto dma_tile = [&](int tile, int slot) {
+    if constexpr (BF16) {
+#pragma unroll
+      for (int d = 0; d < Cfg::kDma; ++d) {
+        const int t = wv + kRingWaves * d;
+        const char* src = item_row(tile, j) + 32 * t + 16 * h;
+        char* dst = stage + slot * Cfg::kTileB + t * 1024;
+        __builtin_amdgcn_global_load_lds((const void*)src, (void*)dst, 16, 0, 0);
+      }
+    }
+  };
+  // fp32: lane units (item j, step u = wv + 4r, half h); raw = their 8 floats
+  constexpr int NUL = Cfg::kUnits > 0 ? Cfg::kUnits : 1;
+  auto load_unit = [&](int tile, uint4 (&raw)[NUL][2]) {
+    if constexpr (!BF16) {
+      const char* row = item_row(tile, j) + 16 * h;
+#pragma unroll
+      for (int r = 0; r < NUL; ++r) {
+        const int u = wv + kRingWaves * r;
+        if (u < NU) {
+          raw[r][0] = *reinterpret_cast<const uint4*>(row + 64 * u);
+          raw[r][1] = *reinterpret_cast<const uint4*>(row + 64 * u + 32);
+        }
+      }
+    }
+  };
+  auto store_pieces = [&](const uint4 (&raw)[NUL][2], int buf) {
+    if constexpr (!BF16) {
+#pragma unroll
+      for (int r = 0; r < NUL; ++r) {
+        const int u = wv + kRingWaves * r;
+        if (u >= NU) continue;
+        const float x[8] = {__uint_as_float(raw[r][0].x), __uint_as_float(raw[r][0].y),
+                            __uint_as_float(raw[r][0].z), __uint_as_float(raw[r][0].w),
+                            __uint_as_float(raw[r][1].x), __uint_as_float(raw[r][1].y),
+                            __uint_as_float(raw[r][1].z), __uint_as_float(raw[r][1].w)};
+        bf16x8 pcs[3];
+        split3x8(x, pcs[0], pcs[1], pcs[2]);
+        char* base = stage + buf * (3 * NU * 1024) + (u * 2 + h) * 512 + j * 16;
+#pragma unroll
+        for (int pc = 0; pc < 3; ++pc)
+          *reinterpret_cast<bf16x8*>(base + pc * NU * 1024) = pcs[pc];
+      }
+    }
+  };
+  // A fragment: bf16 slot/step t, or fp32 piece pc of step u
+  auto a_bf16 = [&](int slot, int t) {
+    return *reinterpret_cast<const bf16x8*>(stage + slot * Cfg::kTileB + (t * 2 + h) * 512 +
+                                            j * 16);
+  };
+  auto a_piece = [&](int buf, int pc, int u) {
+    return *reinterpret_cast<const bf16x8*>(stage + buf * (3 * NU * 1024) + pc * NU * 1024 +
+                                            (u * 2 + h) * 512 + j * 16);
+  };
+  // vmcnt(n): wait until at most n of this wave's vector-memory ops are in flight
+  // (n a compile-time constant; lgkmcnt/expcnt untouched)
+#define HHFM_VMCNT(n) \
+  __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
+
+  uint4 rawA[NUL][2], rawB[NUL][2];
+  float wnext = 0.f;
+  if (tb0 < tb1) {
+    if constexpr (BF16) {
+      for (int s = 0; s < R - 1; ++s) dma_tile(tb0 + s, s);
+    } else {
+      load_unit(tb0, rawA);
+      load_unit(tb0 + 1, rawB);
+      store_pieces(rawA, 0);          // waits for rawA (vmcnt counted by the compiler)
+      load_unit(tb0 + 2, rawA);
+    }
+    if constexpr (FM) {
+      const int item = min(tb0 * kTile + j, N - 1);
+      wnext = w ? w[item_row_begin + item] : 0.f;
+    }
+  }
+
+  auto mma16 = [&](const bf16x8& x, const bf16x8& y, const f32x16& c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+  };
+
+  // one tile: raw sets (cur holds tile+1's unit, nxt receives tile+3's) for fp32
+  auto tile_step = [&](const int tile, uint4 (&cur)[NUL][2], uint4 (&nxt)[NUL][2]) {
+    const int it = tile - tb0;
+    // ---- publish: tile's stage complete and the previous tile's stage free ----
+    if constexpr (BF16) {
+      // DMA of `tile` is older than the (R-2) tiles issued after it
+      HHFM_VMCNT((R - 2) * Cfg::kDma);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's piece stores landed
+    __builtin_amdgcn_s_barrier();
+    if constexpr (BF16) {
+      if (tile + R - 1 < tb1) dma_tile(tile + R - 1, (it + R - 1) % R);
+    } else {
+      // split tile+1 into the other piece buffer, then fetch tile+3's unit
+      if (tile + 1 < tb1) store_pieces(cur, (it + 1) & 1);
+      if (tile + 3 < tb1) load_unit(tile + 3, cur);
+    }
+    (void)nxt;
+    float wcur = wnext;
+    if constexpr (FM) {
+      const int item = min((tile + 1 < tb1 ? tile + 1 : tile) * kTile + j, N - 1);
+      wnext = w ? w[item_row_begin + item] : 0.f;
+    }
+    f32x16 acc = {0};
+    if (HHFM_MAIN_PRIO) __builtin_amdgcn_s_setprio(1);
+    if constexpr (BF16) {
+      const int slot = it % R;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const bf16x8 ai = a_bf16(slot, t);
+        acc = mma16(ai, qp[2][t], acc);
+        acc = mma16(ai, qp[1][t], acc);
+        acc = mma16(ai, qp[0][t], acc);
+      }
+    } else {
+      const int buf = it & 1;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const bf16x8 i0 = a_piece(buf, 0, u), i1 = a_piece(buf, 1, u), i2 = a_piece(buf, 2, u);
+        acc = mma16(i2, qp[0][u], acc);   // smallest terms first (catalog_main order)
+        acc = mma16(i1, qp[1][u], acc);
+        acc = mma16(i0, qp[2][u], acc);
+        acc = mma16(i1, qp[0][u], acc);
+        acc = mma16(i0, qp[1][u], acc);
+        acc = mma16(i0, qp[0][u], acc);
+      }
+    }
+    if (HHFM_MAIN_PRIO) __builtin_amdgcn_s_setprio(0);
+    if constexpr (FM)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f, h == 0 ? 1.f : cq, acc,
+                                                 0, 0, 0);
+    if (!wave_live) return;
+    // ---- filter + insert: catalog_main's selection ----
+    const int ibase = tile * kTile;
+    uint64_t pm[16];
+    if (ibase + kTile <= item_end) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pm[r] = __ballot(acc[r] >= thr);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        pm[r] = __ballot(acc[r] >= thr && ibase + row < item_end);
+      }
+    }
+    int count = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) count += __popcll(pm[r]);
+    if (count == 0) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      uint64_t m = pm[r];
+      while (m) {
+        const int L = __builtin_ctzll(m);
+        m &= m - 1;
+        const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[r]), L));
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (L >> 5);
+        const int qq = L & 31;
+        insert_one<KPAD>(ls + qq * KPAD, li + qq * KPAD, s, ibase + row, K);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (q < B) {
+      const float kth = ls[j * KPAD + (K - 1)];
+      if (kth > thr) {
+        thr = kth;
+        if (h == 0) atomicMax(gthr + q, fkey(kth));
+      }
+    }
+  };
+  for (int tile = tb0; tile < tb1; tile += 2) {
+    tile_step(tile, rawB, rawA);
+    if (tile + 1 < tb1) tile_step(tile + 1, rawA, rawB);
+  }
+#undef HHFM_VMCNT
+  if (!wave_live) return;
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  for (int qq = 0; qq < kQPerWave; ++qq) {
+    const int64_t b = q0 + qq;
+    if (b >= B) break;
+    if (l < K) {
+      const int32_t ii = li[qq * KPAD + l];
+      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * KPAD + l];
+      out_i[b * ostride_b + split * ostride_s + l] = ii == kNoIdx ? kNoIdx : ii + gbase;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 2b. small catalogs (N <= 16,384, e.g. Frappe's 4,082 items): workgroup =
 // 16 waves = 16 queries x one item split.  Per chunk of up to 1,024 items the
 // waves score 16-item x 16-query tiles with v_mfma_f32_16x16x4_f32 (exact
@@ -611,6 +930,7 @@ struct Plan {
   bool dense;            // small catalog, other k: score matrix + dense top-K
   int64_t ldsc;
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
+  int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
       off_seed_i, total;
 };
@@ -664,6 +984,14 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   p.S = (ntiles + p.tiles_per_split - 1) / p.tiles_per_split;
   p.small = small_catalog(B, N, k);
   p.dense = !p.small && dense_catalog(B, N);
+  for (int v = 0; v < 2; ++v) {   // catalog_ring: 2 x 4-wave or 1 x 8-wave workgroups per CU
+    const int nq = 128 << v;
+    p.rnqb[v] = (int)((B + nq - 1) / nq);
+    int rs = ((512 >> v) + p.rnqb[v] - 1) / p.rnqb[v];
+    rs = rs > smax ? smax : (rs < 1 ? 1 : rs);
+    p.rtps[v] = (ntiles + rs - 1) / rs;
+    p.rS[v] = (ntiles + p.rtps[v] - 1) / p.rtps[v];
+  }
   if (p.small) {   // ~2 workgroups per CU; >= 256 items per split
     const int nqg = (int)((B + kSmallQ - 1) / kSmallQ);
     int ss = (512 + nqg - 1) / nqg;
@@ -672,7 +1000,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
     p.ips = (((N + ss - 1) / ss) + 15) & ~15;
     p.Ss = (N + p.ips - 1) / p.ips;
   }
-  const int nsplit = p.small ? p.Ss : p.S;
+  const int nsplit = p.small ? p.Ss : std::max(p.S, std::max(p.rS[0], p.rS[1]));
   size_t off = 0;
   p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
   p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
@@ -739,6 +1067,50 @@ static void launch_main(const Plan& p, const float* H, const float* cst, int64_t
     hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM, false>), dim3(p.nqb * p.S),
                        dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
                        p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
+}
+
+// catalog_ring (K <= 32, bf16 k >= 128 / fp32 k >= 64, split-bf16 MFMA);
+// HHFM_CATALOG_RING=0 keeps catalog_main
+static bool catalog_ring_on() {
+  const char* e = getenv("HHFM_CATALOG_RING");
+  return !(e && e[0] == '0');
+}
+// waves per ring workgroup: HHFM_RING_WAVES=4|8 (default: 4 for bf16, 8 for fp32)
+static int ring_waves(bool bf16) {
+  const char* e = getenv("HHFM_RING_WAVES");
+  if (e && (e[0] == '4' || e[0] == '8')) return e[0] - '0';
+  return bf16 ? 4 : 8;
+}
+
+template <bool BF16, int KT, bool FM>
+static void launch_ring(const Plan& p, const float* H, const float* cst, int64_t B,
+                        const char* E, int64_t item_row_begin, int32_t N, const float* w,
+                        int K, float* os, int32_t* oi, int64_t sb, int64_t ss, int32_t gbase,
+                        int32_t* gthr, hipStream_t st) {
+  if (ring_waves(BF16) == 8)
+    hipLaunchKernelGGL((catalog_ring<BF16, KT, FM, 8>), dim3(p.rnqb[1] * p.rS[1]), dim3(512), 0,
+                       st, H, cst, B, E, item_row_begin, N, w, K, p.rS[1], p.rtps[1], p.rnqb[1],
+                       os, oi, sb, ss, gbase, gthr);
+  else
+    hipLaunchKernelGGL((catalog_ring<BF16, KT, FM, 4>), dim3(p.rnqb[0] * p.rS[0]), dim3(256), 0,
+                       st, H, cst, B, E, item_row_begin, N, w, K, p.rS[0], p.rtps[0], p.rnqb[0],
+                       os, oi, sb, ss, gbase, gthr);
+}
+
+template <bool BF16, bool FM>
+static bool dispatch_ring(int KT, const Plan& p, const float* H, const float* cst, int64_t B,
+                          const char* E, int64_t irb, int32_t N, const float* w, int K,
+                          float* os, int32_t* oi, int64_t sb, int64_t ss, int32_t gbase,
+                          int32_t* gthr, hipStream_t st) {
+  switch (KT) {
+    case 8: launch_ring<BF16, 8, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 16:
+      if constexpr (BF16) return false;
+      else launch_ring<BF16, 16, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st);
+      break;
+    default: return false;
+  }
+  return true;
 }
 
 template <bool BF16, int KPAD, bool FM>
@@ -963,13 +1335,17 @@ extern "C" int hhfm_catalog_topk_ex(
     return (int)hipGetLastError();
   }
 
+  // (bf16 k = 256 would spill at two waves per SIMD: catalog_main keeps it)
+  const bool ring = K <= 32 && p.seed_n > 0 && (bf16 ? KT == 8 : (KT == 8 || KT == 16)) &&
+                    !catalog_exact() && catalog_ring_on();
+  const int S_used = ring ? p.rS[ring_waves(bf16) == 8 ? 1 : 0] : p.S;
   float* os;
   int32_t* oi;
   int64_t sb, ss;
-  if (p.S > 1) {
+  if (S_used > 1) {
     os = reinterpret_cast<float*>(ws + p.off_ps);
     oi = reinterpret_cast<int32_t*>(ws + p.off_pi);
-    sb = (int64_t)p.S * K;
+    sb = (int64_t)S_used * K;
     ss = K;
   } else {
     os = top_score;
@@ -996,7 +1372,10 @@ extern "C" int hhfm_catalog_topk_ex(
                        K, gthr);
   }
 #define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, st
-  if (K <= 32) {
+  if (ring) {
+    if (bf16) ok = fm ? dispatch_ring<true, true>(HHFM_MAIN_ARGS) : dispatch_ring<true, false>(HHFM_MAIN_ARGS);
+    else ok = fm ? dispatch_ring<false, true>(HHFM_MAIN_ARGS) : dispatch_ring<false, false>(HHFM_MAIN_ARGS);
+  } else if (K <= 32) {
     if (bf16) ok = fm ? dispatch_kt<true, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<true, 32, false>(HHFM_MAIN_ARGS);
     else ok = fm ? dispatch_kt<false, 32, true>(HHFM_MAIN_ARGS) : dispatch_kt<false, 32, false>(HHFM_MAIN_ARGS);
   } else {
@@ -1005,8 +1384,8 @@ extern "C" int hhfm_catalog_topk_ex(
   }
 #undef HHFM_MAIN_ARGS
   if (!ok) return HHFM_EUNSUPPORTED;
-  if (p.S > 1) {
-    launch_merge(os, oi, p.S, B, K, /*stride_r=*/K, /*stride_b=*/(int64_t)p.S * K,
+  if (S_used > 1) {
+    launch_merge(os, oi, S_used, B, K, /*stride_r=*/K, /*stride_b=*/(int64_t)S_used * K,
                  top_score, top_idx, st);
   }
   return (int)hipGetLastError();
