@@ -30,6 +30,17 @@
 // All LDS is one __shared__ object: a second object beside the LDS-DMA
 // target makes hipcc drain the DMA (vmcnt(0)) before LDS reads.
 //
+// Projected layer 0 (PROJ = true).  Layer 0 is linear before its ReLU and
+// row m's input is the concat of F table rows, so
+//   h_0[m] = Σ_f W0[:, f·k:(f+1)·k] · E[x_f]  =  Σ_f P_f[x_f]
+// with P_f[id] = W0_f · E[id] computed ONCE per call for every table row
+// (dfm_project_layer0: F MFMA GEMMs [M, k] x [k, N0], the same bf16-rounded
+// operands / exact-fp32 products as the direct kernel, fp32 results).  When
+// the rows outnumber the table rows (rows >= 2·M; C5 scores 12.5 M rows
+// against 5,051 table rows) this removes layer 0's MFMA work (61 % of C5's
+// FLOPs) and its weight stream: the kernel gathers F rows of P per row
+// straight into the accumulator layout and runs the hidden layers as before.
+//
 // out[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c]) + bp) + Σ_n relu(h_L)·Wp[F+k+n]
 #include "gemm_mfma.h"
 
@@ -60,6 +71,9 @@ struct FusedDfmArgs {
   float bp;
   float* out;
   const uint4* packed;   // chunk sequence written by dfm_pack_weights
+  const float* proj;     // PROJ: P_f[id][n] at proj + f·proj_fstride + id·proj_ld + n
+  int64_t proj_fstride;
+  int proj_ld;           // 32·TM (zero beyond dims[0])
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -106,7 +120,7 @@ __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, 
   }
 }
 
-template <bool TBF, int TM>
+template <bool TBF, int TM, bool PROJ>
 __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   constexpr int NR = TM * 32;                // weight rows per chunk
   constexpr int CU = NR * 8;                 // 16-B units per chunk
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   const int64_t m0 = (int64_t)blockIdx.x * kFusedRows;
   const int F = a.F, k = a.k, L = a.L;
   const int nS = F * (k / 16);               // layer-0 k16 steps
-  const int nc0 = (nS + 3) / 4;              // layer-0 K-chunks
+  const int nc0 = PROJ ? 0 : (nS + 3) / 4;   // layer-0 K-chunks (none when projected)
   const int nchunks = nc0 + (L - 1) * NC;
 
   for (int x = tid; x < kFusedRows * F; x += 256) {
@@ -203,18 +217,12 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   float y2 = 0.f;
 
   __syncthreads();   // ids, step tables visible
-  EChunk e0, e1;
-  Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
-  eload(e0, cg);
-  dma(0, 0);
-  __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
   // Per K-chunk g (buffer g&1): DMA chunk g+1 into the other buffer (read in
   // chunk g-1, released by its barrier), load the next embedding chunk into
   // the other register set, run chunk g's MFMAs, then vmcnt(0) + barrier
   // (__syncthreads) publishes chunk g+1.
 
-  // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
   // One 64-deep chunk from LDS buffer b: the TM weight fragments of step
   // j+1 are read right behind step j's MFMAs (software pipelined; one wave
   // per SIMD has no other wave to hide LDS latency), bop(j) supplies the B
@@ -235,6 +243,73 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
       side(j);
     }
   };
+
+  if constexpr (PROJ) {
+    // ----- projected layer 0: acc = Σ_f P_f[x_f], FM part from the table -----
+    if (nchunks > 0) dma(0, 0);   // first hidden chunk streams behind the gathers
+    // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
+    // one float4 of P per (field, tile, g); all 4·TM of a field in flight
+    for (int f = 0; f < F; ++f) {
+      const float4* pp = reinterpret_cast<const float4*>(
+                             a.proj + f * a.proj_fstride +
+                             (int64_t)ids[myrow * F + f] * a.proj_ld) + h;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 x = pp[8 * t + 2 * g4];
+          acc[t][4 * g4 + 0] += x.x;
+          acc[t][4 * g4 + 1] += x.y;
+          acc[t][4 * g4 + 2] += x.z;
+          acc[t][4 * g4 + 3] += x.w;
+        }
+    }
+    // FM second-order part (DFM.py:114-122): the lane half h takes columns
+    // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
+    for (int j = 0; j < k / 16; ++j) {
+      float s8[8], q8[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) { s8[q] = 0.f; q8[q] = 0.f; }
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = ids[myrow * F + f];
+        float v[8];
+        if constexpr (TBF) {
+          const uint4 x = *reinterpret_cast<const uint4*>(
+              reinterpret_cast<const uint16_t*>(a.E) + id * k + 16 * j + 8 * h);
+          const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] = __uint_as_float(x4[q] << 16);
+            v[2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
+          }
+        } else {
+          const float4* p = reinterpret_cast<const float4*>(
+              reinterpret_cast<const float*>(a.E) + id * k + 16 * j + 8 * h);
+          const float4 p0 = p[0], p1 = p[1];
+          v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
+          v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          s8[q] += v[q];
+          q8[q] += v[q] * v[q];
+        }
+      }
+      const float4* wc = reinterpret_cast<const float4*>(wpl + kFusedMaxF + 16 * j + 8 * h);
+      const float4 w0 = wc[0], w1 = wc[1];
+      const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) d += 0.5f * (s8[q] * s8[q] - q8[q]) * wq[q];
+      y2 += d;
+    }
+    __syncthreads();   // vmcnt(0): hidden chunk 0 landed
+  } else {
+  EChunk e0, e1;
+  Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
+  eload(e0, cg);
+  dma(0, 0);
+  __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
   // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
   // Chunk c first turns the embeddings gathered during chunk c-1 into its 4
@@ -308,6 +383,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     chunk0(c, e0, e1);
     if (c + 1 < nc0) chunk0(c + 1, e1, e0);
   }
+  }   // direct layer 0
 
   // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
   uint32_t X[TM][8];
@@ -420,7 +496,7 @@ __global__ __launch_bounds__(256) void dfm_pack_weights_f32(FusedDfmArgs a, int 
   }
 }
 
-template <bool TBF, int TM>
+template <bool TBF, int TM, bool PROJ>
 __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
   constexpr int NR = TM * 32;
   constexpr int T16 = 2 * TM;                // 16-unit output tiles
@@ -445,7 +521,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
   const int64_t m0 = (int64_t)blockIdx.x * kF32Rows;
   const int F = a.F, k = a.k, L = a.L;
   const int nB = F * (k / 16);
-  const int nc0 = (nB + 1) / 2;
+  const int nc0 = PROJ ? 0 : (nB + 1) / 2;
   const int nchunks = nc0 + (L - 1) * TM;
 
   for (int x = tid; x < kF32Rows * F; x += 256) {
@@ -509,10 +585,6 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
   float y2 = 0.f;
 
   __syncthreads();
-  EChunk ea, eb;
-  eload(ea, 0);
-  dma(0, 0);
-  __syncthreads();
 
   // one 16-k step (weight units 4s..4s+3 of the chunk; lane group kq takes
   // unit 4s+kq): 4 MFMAs per output tile, next tile's fragment read ahead
@@ -528,6 +600,58 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.w, bv[3], acc[t], 0, 0, 0);
     }
   };
+
+  if constexpr (PROJ) {
+    // ----- projected layer 0: acc = Σ_f P_f[x_f] (16x16 C/D map: lane group
+    // kq holds units 16t + 4kq .. +3 of its row), FM part from the table -----
+    if (nchunks > 0) dma(0, 0);
+    for (int f = 0; f < F; ++f) {
+      const float4* pp = reinterpret_cast<const float4*>(
+                             a.proj + f * a.proj_fstride +
+                             (int64_t)ids[myrow * F + f] * a.proj_ld) + kq;
+#pragma unroll
+      for (int t = 0; t < T16; ++t) {
+        const float4 x = pp[4 * t];
+        acc[t][0] += x.x;
+        acc[t][1] += x.y;
+        acc[t][2] += x.z;
+        acc[t][3] += x.w;
+      }
+    }
+    // FM second-order part (DFM.py:114-122), columns 16j + 4kq .. +3 of every
+    // 16-column block j, summed as the direct kernel does
+    for (int j = 0; j < k / 16; ++j) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) { fs[x] = 0.f; fq[x] = 0.f; }
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = ids[myrow * F + f];
+        float bv[4];
+        if constexpr (TBF) {
+          const uint2 x = *reinterpret_cast<const uint2*>(
+              reinterpret_cast<const uint16_t*>(a.E) + id * k + 16 * j + 4 * kq);
+          bv[0] = __uint_as_float(x.x << 16); bv[1] = __uint_as_float(x.x & 0xffff0000u);
+          bv[2] = __uint_as_float(x.y << 16); bv[3] = __uint_as_float(x.y & 0xffff0000u);
+        } else {
+          const float4 x = *reinterpret_cast<const float4*>(
+              reinterpret_cast<const float*>(a.E) + id * k + 16 * j + 4 * kq);
+          bv[0] = x.x; bv[1] = x.y; bv[2] = x.z; bv[3] = x.w;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          fs[x] += bv[x];
+          fq[x] += bv[x] * bv[x];
+        }
+      }
+      const float* wc = wpl + F + 16 * j + 4 * kq;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) y2 += 0.5f * (fs[x] * fs[x] - fq[x]) * wc[x];
+    }
+    __syncthreads();   // vmcnt(0): hidden chunk 0 landed
+  } else {
+  EChunk ea, eb;
+  eload(ea, 0);
+  dma(0, 0);
+  __syncthreads();
 
   // ----- layer 0 -----
   auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
@@ -562,6 +686,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
     chunk0(c, ea, eb);
     if (c + 1 < nc0) chunk0(c + 1, eb, ea);
   }
+  }   // direct layer 0
 
   // ----- layers 1..L-1: the previous layer's fp32 output is the B operand -----
   f32x4 X[T16];
@@ -639,11 +764,64 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16) {
   return (size_t)(nc0 + (L - 1) * nch) * 32 * TM * 8 * 16;
 }
 
-// returns false when the shape is outside the fused kernel's envelope
+// ---------------------------------------------------------------------------
+// Projected layer 0: P_f[id] = W0[:, f·k:(f+1)·k] · E[id] for every table row
+// id and field f, fp32, row stride 32·TM (columns >= dims[0] zero).  F MFMA
+// GEMMs [M, k] x [k, N0] on the shared tile kernel, A = the table through an
+// identity gather (fp32 tables rounded to bf16 exactly like the direct
+// kernel's B operand; bf16 MFMA with fp32 accumulation, or exact fp32 MFMA for
+// the fp32 MLP).  Workspace: [P: F·M·ld floats][identity ids: M int32].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dfm_iota(int32_t* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int32_t)i;
+}
+
+bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims) {
+  return dfm_fused_eligible(L, dims) && F >= 1 && F <= kFusedMaxF && k % 16 == 0 &&
+         k <= kFusedMaxK;
+}
+
+int dfm_proj_ld(int L, const int32_t* dims) { return 32 * fused_tm(fused_max_tiles(L, dims)); }
+
+size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims) {
+  const size_t p = (size_t)F * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
+  return ((p + 255) & ~size_t(255)) + (((size_t)M * 4 + 255) & ~size_t(255));
+}
+
+void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
+                        const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
+                        hipStream_t st) {
+  const int ld = dfm_proj_ld(L, dims);
+  const size_t pbytes = ((size_t)F * M * ld * 4 + 255) & ~size_t(255);
+  float* P = reinterpret_cast<float*>(ws);
+  int32_t* iota = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + pbytes);
+  const int64_t ib = (M + 255) / 256 < 4096 ? (M + 255) / 256 : 4096;
+  hipLaunchKernelGGL(dfm_iota, dim3((unsigned)ib), dim3(256), 0, st, iota, M);
+  const int ldb0 = (F * k + 7) & ~7;
+  const size_t esz = mlp_bf16 ? 2 : 4;
+  for (int f = 0; f < F; ++f) {
+    GemmArgs g{};
+    g.M = M;
+    g.N = N0;
+    g.K = k;
+    g.gidx = iota; g.T = E; g.Mtab = M; g.F = 1; g.kf = k; g.t_bf16 = tbf;
+    g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)f * k * esz;
+    g.ldb = ldb0;
+    g.relu = 0;
+    g.C = P + (size_t)f * M * ld;
+    g.ldc = ld;
+    launch_gemm(g, mlp_bf16, 0, st);
+  }
+}
+
+// returns false when the shape is outside the fused kernel's envelope.
+// proj != nullptr: layer 0 from dfm_project_layer0's workspace (PROJ kernels).
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, hipStream_t st) {
+                      float* out, void* pack_ws, const float* proj, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -661,17 +839,27 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   }
   a.Wp = Wp; a.bp = bp; a.out = out;
   a.packed = reinterpret_cast<const uint4*>(pack_ws);
+  a.proj = proj;
+  a.proj_ld = 32 * TM;
+  a.proj_fstride = (int64_t)M * a.proj_ld;
+  const bool pj = proj != nullptr;
   if (!mlp_bf16) {
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
-    const int nc0 = (F * (k / 16) + 1) / 2;
+    const int nc0 = pj ? 0 : (F * (k / 16) + 1) / 2;
     const int64_t units = (int64_t)(nc0 + (L - 1) * TM) * 32 * TM * 8;
     const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
-    hipLaunchKernelGGL(dfm_pack_weights_f32, dim3(pblocks), dim3(256), 0, st, a, TM, nc0,
-                       reinterpret_cast<uint4*>(pack_ws));
-#define HHFM_FUSED32(T)                                                                  \
-  case T:                                                                                \
-    if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T>), grid, dim3(256), 0, st, a);    \
-    else hipLaunchKernelGGL((dfm_fused_f32<false, T>), grid, dim3(256), 0, st, a);       \
+    if (units > 0)
+      hipLaunchKernelGGL(dfm_pack_weights_f32, dim3(pblocks), dim3(256), 0, st, a, TM, nc0,
+                         reinterpret_cast<uint4*>(pack_ws));
+#define HHFM_FUSED32(T)                                                                    \
+  case T:                                                                                  \
+    if (pj) {                                                                              \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, true>), grid, dim3(256), 0, st, a);  \
+      else hipLaunchKernelGGL((dfm_fused_f32<false, T, true>), grid, dim3(256), 0, st, a);     \
+    } else {                                                                               \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, false>), grid, dim3(256), 0, st, a); \
+      else hipLaunchKernelGGL((dfm_fused_f32<false, T, false>), grid, dim3(256), 0, st, a);    \
+    }                                                                                      \
     break;
     switch (TM) {
       HHFM_FUSED32(2)
@@ -687,15 +875,21 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     return true;
   }
   const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
-  const int nS = F * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;
+  const int nS = F * (k / 16), nc0 = pj ? 0 : (nS + 3) / 4, NC = (TM + 1) / 2;
   const int64_t units = (int64_t)(nc0 + (L - 1) * NC) * 32 * TM * 8;
   const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
-  hipLaunchKernelGGL(dfm_pack_weights, dim3(pblocks), dim3(256), 0, st, a, TM, nc0, NC,
-                     reinterpret_cast<uint4*>(pack_ws));
-#define HHFM_FUSED(T)                                                                    \
-  case T:                                                                                \
-    if (tbf) hipLaunchKernelGGL((dfm_fused<true, T>), grid, dim3(256), 0, st, a);        \
-    else hipLaunchKernelGGL((dfm_fused<false, T>), grid, dim3(256), 0, st, a);           \
+  if (units > 0)
+    hipLaunchKernelGGL(dfm_pack_weights, dim3(pblocks), dim3(256), 0, st, a, TM, nc0, NC,
+                       reinterpret_cast<uint4*>(pack_ws));
+#define HHFM_FUSED(T)                                                                      \
+  case T:                                                                                  \
+    if (pj) {                                                                              \
+      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, true>), grid, dim3(256), 0, st, a);      \
+      else hipLaunchKernelGGL((dfm_fused<false, T, true>), grid, dim3(256), 0, st, a);         \
+    } else {                                                                               \
+      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, false>), grid, dim3(256), 0, st, a);     \
+      else hipLaunchKernelGGL((dfm_fused<false, T, false>), grid, dim3(256), 0, st, a);        \
+    }                                                                                      \
     break;
   switch (TM) {
     HHFM_FUSED(2)

@@ -29,7 +29,12 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, hipStream_t st);
+                      float* out, void* pack_ws, const float* proj, hipStream_t st);
+bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
+size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims);
+void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
+                        const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
+                        hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // FM part of DeepFM and the final reduce
@@ -95,17 +100,32 @@ __global__ __launch_bounds__(256) void dfm_build_rows(const int32_t* __restrict_
 
 
 // workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL][packed weights of
-// the fused bf16 kernel, when its envelope admits the layer widths]
+// the fused kernels, when their envelope admits the layer widths][projected
+// layer 0 (dfm_fused.hip), when planned]
 struct DfmPlan {
-  size_t off_base, off_part, off_h0, off_h1, off_pack, total;
+  size_t off_base, off_part, off_h0, off_h1, off_pack, off_proj, total;
   int maxL, ntl;
+  bool proj;
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 // activations / weights keep their K dimension padded to 8 (16-B rows)
 static int pad8(int x) { return (x + 7) & ~7; }
 
-static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype) {
+// Projected layer 0 (dfm_fused.hip): at most this much workspace for P.
+constexpr size_t kProjMaxBytes = size_t(1) << 30;
+
+// proj_mode: HHFM_DFM_PROJ_OFF plans no projection (F, k, M unused);
+// HHFM_DFM_PROJ_ON plans it whenever the fused kernels admit the shape and P
+// fits kProjMaxBytes; HHFM_DFM_PROJ_AUTO additionally needs the fp32 MLP and
+// rows_total >= 2·M (P costs one layer-0 row per table row and field).  With
+// the bf16 MLP the P gather (F·32·TM fp32 per row, table-row-random) costs
+// what the bf16 layer-0 MFMAs it removes cost — C5: 4.75 ms projected vs
+// 4.72 direct per 2 M rows — so AUTO leaves it direct; with the fp32 MLP
+// (16x slower MFMA) it halves C5 (17.2 vs 35.2 ms).
+static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype, int F = 0,
+                        int k = 0, int64_t M = 0, int64_t rows_total = 0,
+                        int proj_mode = HHFM_DFM_PROJ_OFF) {
   DfmPlan p{};
   p.maxL = 0;
   for (int i = 0; i < nlayers; ++i) p.maxL = pad8(dims[i]) > p.maxL ? pad8(dims[i]) : p.maxL;
@@ -119,6 +139,15 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   p.off_pack = off;
   if (dfm_fused_eligible(nlayers, dims))
     off += al256(dfm_fused_pack_bytes(nlayers, dims, mlp_dtype == HHFM_BF16));
+  p.off_proj = off;
+  if (proj_mode != HHFM_DFM_PROJ_OFF && M > 0 && dfm_proj_eligible(F, k, nlayers, dims) &&
+      (proj_mode == HHFM_DFM_PROJ_ON || (mlp_dtype == HHFM_F32 && rows_total >= 2 * M))) {
+    const size_t pb = dfm_proj_bytes(F, M, nlayers, dims);
+    if (pb <= kProjMaxBytes) {
+      p.proj = true;
+      off += al256(pb);
+    }
+  }
   p.total = off;
   return p;
 }
@@ -136,11 +165,13 @@ static int dfm_check(int64_t B, int32_t F, int32_t k, int32_t dtype, int32_t nla
   return HHFM_OK;
 }
 
+// proj: P from dfm_project_layer0 (the fused PROJ kernels then run), or null
 static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void* E,
                             int64_t M, int32_t k, int32_t dtype, const float* w,
                             int32_t nlayers, const int32_t* dims, const void* const* Wt,
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
-                            float bp, float* out, char* ws, const DfmPlan& p, hipStream_t st) {
+                            float bp, float* out, char* ws, const DfmPlan& p, const float* proj,
+                            hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
   // One fused kernel per 128-row block when the shape fits (dfm_fused.hip,
   // bf16 or fp32 MLP); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
@@ -148,10 +179,11 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
     const char* e = getenv("HHFM_DFM_LAYERED");
     return e && e[0] == '1';
   }();
-  if (!layered && p.total > p.off_pack &&
+  if ((proj || !layered) && p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
-                       Wp, bp, out, ws + p.off_pack, st))
+                       Wp, bp, out, ws + p.off_pack, proj, st))
     return (int)hipGetLastError();
+  if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);
   float* part = reinterpret_cast<float*>(ws + p.off_part);
   void* h[2] = {ws + p.off_h0, ws + p.off_h1};
@@ -205,6 +237,19 @@ extern "C" int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int3
   return HHFM_OK;
 }
 
+extern "C" int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k,
+                                             int64_t features_M, int32_t nlayers,
+                                             const int32_t* layer_dims, int32_t mlp_dtype,
+                                             int32_t proj_mode, size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 1 || k < 1 || features_M < 1 || nlayers < 1 || !layer_dims)
+    return HHFM_EINVAL;
+  if (proj_mode != HHFM_DFM_PROJ_OFF && proj_mode != HHFM_DFM_PROJ_ON &&
+      proj_mode != HHFM_DFM_PROJ_AUTO)
+    return HHFM_EINVAL;
+  *ws_bytes = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode).total;
+  return HHFM_OK;
+}
+
 extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
                                 int64_t features_M, int32_t k, int32_t dtype, const float* w,
                                 int32_t nlayers, const int32_t* layer_dims,
@@ -218,11 +263,20 @@ extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const 
   if (!idx || !E || !w || !Wt || !bias || !Wp || !out) return HHFM_EINVAL;
   for (int i = 0; i < nlayers; ++i)
     if (!Wt[i] || !bias[i]) return HHFM_EINVAL;
-  const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype);
+  // the projected layer 0 runs when the workspace holds its plan
+  DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, HHFM_DFM_PROJ_ON);
+  if (!p.proj || !workspace || ws_bytes < p.total) p = dfm_plan(B, nlayers, layer_dims, mlp_dtype);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
+  char* ws = reinterpret_cast<char*>(workspace);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float* proj = nullptr;
+  if (p.proj) {
+    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
+                       layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
+    proj = reinterpret_cast<const float*>(ws + p.off_proj);
+  }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
-                          mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
-                          reinterpret_cast<hipStream_t>(stream));
+                          mlp_dtype, Wp, bp, out, ws, p, proj, st);
 }
 
 // D2: chunk_rows bounds the rows (queries x items) scored per forward pass.
@@ -233,6 +287,10 @@ static int64_t dfm_cat_qchunk(int64_t B, int32_t N, int64_t chunk_rows) {
   return qc;
 }
 
+static size_t dfm_cat_bytes(const DfmPlan& p, int64_t rows, int F) {
+  return p.total + al256((size_t)rows * F * 4) + al256((size_t)rows * 4);
+}
+
 extern "C" int hhfm_dfm_catalog_topk_workspace(int64_t B, int32_t F, int32_t item_count,
                                                int32_t nlayers, const int32_t* layer_dims,
                                                int32_t mlp_dtype, int64_t chunk_rows,
@@ -240,8 +298,26 @@ extern "C" int hhfm_dfm_catalog_topk_workspace(int64_t B, int32_t F, int32_t ite
   if (!ws_bytes || B < 0 || F < 1 || item_count < 1 || chunk_rows < 1) return HHFM_EINVAL;
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
-  const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
-  *ws_bytes = p.total + al256((size_t)rows * F * 4) + al256((size_t)rows * 4);
+  *ws_bytes = dfm_cat_bytes(dfm_plan(rows, nlayers, layer_dims, mlp_dtype), rows, F);
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_dfm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t k,
+                                                  int64_t features_M, int32_t item_count,
+                                                  int32_t nlayers, const int32_t* layer_dims,
+                                                  int32_t mlp_dtype, int64_t chunk_rows,
+                                                  int32_t proj_mode, size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 1 || k < 1 || features_M < 1 || item_count < 1 ||
+      chunk_rows < 1 || nlayers < 1 || !layer_dims)
+    return HHFM_EINVAL;
+  if (proj_mode != HHFM_DFM_PROJ_OFF && proj_mode != HHFM_DFM_PROJ_ON &&
+      proj_mode != HHFM_DFM_PROJ_AUTO)
+    return HHFM_EINVAL;
+  const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
+  const int64_t rows = qc * item_count;
+  const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
+                             B * (int64_t)item_count, proj_mode);
+  *ws_bytes = dfm_cat_bytes(p, rows, F);
   return HHFM_OK;
 }
 
@@ -265,13 +341,21 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   if (!qidx || !E || !w || !Wt || !bias || !Wp || !top_score || !top_idx) return HHFM_EINVAL;
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
-  const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
-  const size_t need = p.total + al256((size_t)rows * F * 4) + al256((size_t)rows * 4);
-  if (!workspace || ws_bytes < need) return HHFM_EWORKSPACE;
+  DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
+                       B * (int64_t)item_count, HHFM_DFM_PROJ_ON);
+  if (!p.proj || !workspace || ws_bytes < dfm_cat_bytes(p, rows, F))
+    p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
+  if (!workspace || ws_bytes < dfm_cat_bytes(p, rows, F)) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   int32_t* rbuf = reinterpret_cast<int32_t*>(ws + p.total);
   float* sc = reinterpret_cast<float*>(ws + p.total + al256((size_t)rows * F * 4));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float* proj = nullptr;
+  if (p.proj) {   // once per call: every query chunk reuses it
+    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
+                       layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
+    proj = reinterpret_cast<const float*>(ws + p.off_proj);
+  }
   for (int64_t b0 = 0; b0 < B; b0 += qc) {
     const int64_t nb = (B - b0) < qc ? (B - b0) : qc;
     const int64_t nrows = nb * item_count;
@@ -280,7 +364,7 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
     hipLaunchKernelGGL(dfm_build_rows, dim3((unsigned)blocks), dim3(256), 0, st, qidx + b0 * F,
                        nb, F, item_col, item_row_begin, item_count, rbuf);
     rc = dfm_forward_impl(rbuf, nrows, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
-                          bias, mlp_dtype, Wp, bp, sc, ws, p, st);
+                          bias, mlp_dtype, Wp, bp, sc, ws, p, proj, st);
     if (rc) return rc;
     launch_topk_dense(sc, nb, item_count, item_count, K, global_item_base, top_score + b0 * K,
                       top_idx + b0 * K, st);

@@ -212,6 +212,16 @@ PYBIND11_MODULE(_hhfm, m) {
           return ws;
         });
 
+  m.def("dfm_forward_workspace_ex",
+        [](int64_t B, int F, int k, int64_t M, std::vector<int32_t> dims, int mlp_dtype,
+           int proj_mode) {
+          size_t ws = 0;
+          check(hhfm_dfm_forward_workspace_ex(B, F, k, M, (int)dims.size(), dims.data(),
+                                              mlp_dtype, proj_mode, &ws),
+                "hhfm_dfm_forward_workspace_ex");
+          return ws;
+        });
+
   m.def("dfm_forward",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w,
            std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
@@ -243,6 +253,17 @@ PYBIND11_MODULE(_hhfm, m) {
           check(hhfm_dfm_catalog_topk_workspace(B, F, item_count, (int)dims.size(), dims.data(),
                                                 mlp_dtype, chunk_rows, &ws),
                 "hhfm_dfm_catalog_topk_workspace");
+          return ws;
+        });
+
+  m.def("dfm_catalog_topk_workspace_ex",
+        [](int64_t B, int F, int k, int64_t M, int item_count, std::vector<int32_t> dims,
+           int mlp_dtype, int64_t chunk_rows, int proj_mode) {
+          size_t ws = 0;
+          check(hhfm_dfm_catalog_topk_workspace_ex(B, F, k, M, item_count, (int)dims.size(),
+                                                   dims.data(), mlp_dtype, chunk_rows, proj_mode,
+                                                   &ws),
+                "hhfm_dfm_catalog_topk_workspace_ex");
           return ws;
         });
 

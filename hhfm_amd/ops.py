@@ -214,10 +214,17 @@ def dfm_prepare_weights(layers, biases, mlp_dtype: torch.dtype, F: int, k: int):
     return Wt, bs, dims
 
 
+DFM_PROJ = {False: 0, True: 1, None: 2}   # include/hhfm.h hhfm_dfm_proj: off / on / auto
+
+
 def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                 mlp_dtype: torch.dtype, Wp: torch.Tensor, bp: float,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B]."""
+                out: Optional[torch.Tensor] = None,
+                proj: Optional[bool] = None) -> torch.Tensor:
+    """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B].
+
+    ``proj``: projected layer 0 (include/hhfm.h, ABI v3) — None lets the
+    library decide (rows >= 2 x table rows), True / False force it on / off."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, Wp, *Wt, *bias)
     B, F = idx.shape
@@ -228,10 +235,13 @@ def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, d
     if out is None:
         out = torch.empty(B, dtype=torch.float32, device=dev)
     nat = native()
-    ws = _workspace(dev, nat.dfm_forward_workspace(B, list(dims), md))
+    nbytes = nat.dfm_forward_workspace_ex(B, F, k, M, list(dims), md, DFM_PROJ[proj])
+    ws = _workspace(dev, nbytes)
+    # the planned size, not the (cached, possibly larger) buffer's: the
+    # library picks the projected path from the size it is handed
     nat.dfm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
                     list(dims), [t.data_ptr() for t in Wt], [t.data_ptr() for t in bias], md,
-                    Wp.data_ptr(), float(bp), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                    Wp.data_ptr(), float(bp), out.data_ptr(), ws.data_ptr(), nbytes,
                     _stream(dev))
     return out
 
@@ -239,23 +249,25 @@ def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, d
 def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                      Wp: torch.Tensor, bp: float, item_col: int, item_row_begin: int,
                      item_count: int, K: int, global_item_base: int = 0,
-                     chunk_rows: int = 1 << 20):
-    """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K])."""
+                     chunk_rows: int = 1 << 20, proj: Optional[bool] = None):
+    """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K]); ``proj`` as
+    in :func:`dfm_forward` (rows = B x item_count)."""
     _idx(qidx, "qidx")
     dev = _need_cuda(qidx, E, w, Wp, *Wt, *bias)
     B, F = qidx.shape
     M, k = E.shape
     md = _dtype_code(Wt[0])
     nat = native()
-    ws = _workspace(dev, nat.dfm_catalog_topk_workspace(B, F, item_count, list(dims), md,
-                                                        chunk_rows))
+    nbytes = nat.dfm_catalog_topk_workspace_ex(B, F, k, M, item_count, list(dims), md,
+                                               chunk_rows, DFM_PROJ[proj])
+    ws = _workspace(dev, nbytes)
     top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
     top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
     nat.dfm_catalog_topk(qidx.data_ptr(), B, F, item_col, E.data_ptr(), M, k, _dtype_code(E),
                          w.data_ptr(), list(dims), [t.data_ptr() for t in Wt],
                          [t.data_ptr() for t in bias], md, Wp.data_ptr(), float(bp),
                          item_row_begin, item_count, global_item_base, K, chunk_rows,
-                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), ws.numel(),
+                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), nbytes,
                          _stream(dev))
     return top_s, top_i
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HHFM_ABI_VERSION 2
+#define HHFM_ABI_VERSION 3
 
 enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 
@@ -174,6 +174,27 @@ int hhfm_topk_merge_host(const float* in_score, const int32_t* in_idx,
  * ---------------------------------------------------------------------- */
 int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_dims,
                                int32_t mlp_dtype, size_t* ws_bytes);
+
+/* Projected layer 0 (ABI v3).  Layer 0 is linear before its ReLU, so
+ * h_0 = Σ_f P_f[x_f] with P_f[id] = W0[:, f·k:(f+1)·k] · E[id]: the forward
+ * computes P for every table row and field once per call (F MFMA GEMMs, the
+ * direct kernel's operand rounding) and the fused kernel gathers it instead
+ * of streaming layer 0's weights — a saving when rows >= 2·features_M
+ * (DFM.py:125-128 computed by the same products, summed per field first).
+ * hhfm_dfm_forward / hhfm_dfm_catalog_topk take that path when ws_bytes
+ * covers the projected plan (the *_workspace_ex size with proj_mode != OFF)
+ * and the shape is inside the fused envelope (k % 16 == 0, k <= 512, F <= 16,
+ * <= 4 layers of <= 416 units); otherwise the direct kernels run.
+ * P needs F·features_M·32·⌈max width/32⌉ floats (at most 1 GiB planned). */
+enum hhfm_dfm_proj {
+  HHFM_DFM_PROJ_OFF = 0,  /* plan the direct path only                       */
+  HHFM_DFM_PROJ_ON = 1,   /* plan P whenever the shape admits it             */
+  HHFM_DFM_PROJ_AUTO = 2  /* plan P for the fp32 MLP when rows (B, or
+                             B·item_count) >= 2·M; bf16 MLP stays direct     */
+};
+int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k, int64_t features_M,
+                                  int32_t nlayers, const int32_t* layer_dims,
+                                  int32_t mlp_dtype, int32_t proj_mode, size_t* ws_bytes);
 int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
                      int64_t features_M, int32_t k, int32_t dtype, const float* w,
                      int32_t nlayers, const int32_t* layer_dims, const void* const* Wt,
@@ -188,6 +209,11 @@ int hhfm_dfm_catalog_topk_workspace(int64_t B, int32_t F, int32_t item_count,
                                     int32_t nlayers, const int32_t* layer_dims,
                                     int32_t mlp_dtype, int64_t chunk_rows,
                                     size_t* ws_bytes);
+int hhfm_dfm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t k,
+                                       int64_t features_M, int32_t item_count,
+                                       int32_t nlayers, const int32_t* layer_dims,
+                                       int32_t mlp_dtype, int64_t chunk_rows,
+                                       int32_t proj_mode, size_t* ws_bytes);
 int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
                           const void* E, int64_t features_M, int32_t k, int32_t dtype,
                           const float* w, int32_t nlayers, const int32_t* layer_dims,

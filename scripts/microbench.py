@@ -107,18 +107,28 @@ if not only or "dfm" in only:
             (torch.float32, torch.float32, "dfm_c5_f32")]
     if os.environ.get("MB_DFM_LEGS"):
         legs = [x for x in legs if x[2] in os.environ["MB_DFM_LEGS"].split(",")]
+    # MB_DFM_PROJ: "0" direct layer 0 only, "1" projected only, default both
+    projs = {"0": [False], "1": [True]}.get(os.environ.get("MB_DFM_PROJ", ""), [False, True])
     for mdt, tdt, name in legs:
         m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
                    mlp_dtype=mdt, table_dtype=tdt)
         m.validate = False
         Wt, bs, dims, Wp, bp = m._prepared()
-        out = torch.empty(B, device=dev)
-        fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,  # noqa
-                                     dims, mdt, Wp, bp, out=out)
-        med, mn = timeit(fn, reps=5)
-        res[name] = {"median_ms": med, "rows_per_s": B / (med * 1e-3),
-                     "TFLOPs": flops_row * B / (med * 1e-3) / 1e12}
-        del m
+        outs = {}
+        for pj in projs:
+            out = torch.empty(B, device=dev)
+            fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1),  # noqa
+                                         Wt, bs, dims, mdt, Wp, bp, out=out, proj=pj)
+            med, mn = timeit(fn, reps=5)
+            leg = name + ("_proj" if pj else "")
+            res[leg] = {"median_ms": med, "rows_per_s": B / (med * 1e-3),
+                        "TFLOPs_reference_flops": flops_row * B / (med * 1e-3) / 1e12}
+            outs[pj] = out
+        if len(outs) == 2:
+            d = (outs[True] - outs[False]).abs().max().item()
+            res[name + "_proj"]["max_abs_diff_vs_direct"] = d
+            res[name + "_proj"]["out_abs_max"] = outs[False].abs().max().item()
+        del m, outs
         torch.cuda.empty_cache()
 
 if not only or "afm" in only:

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     lib.hhfm_abi_version.restype = ctypes.c_int
-    assert lib.hhfm_abi_version() == 2
+    assert lib.hhfm_abi_version() == 3
 
 
 def test_pybind_module_binds_the_abi():
@@ -36,7 +36,7 @@ def test_pybind_module_binds_the_abi():
               "topk_merge", "topk_merge_host", "check_ids", "status_read",
               "probe_stream_read"]:
         assert hasattr(m, n)
-    assert m.abi_version() == 2
+    assert m.abi_version() == 3
 
 
 def test_argument_validation_without_device():
@@ -158,3 +158,24 @@ def test_wide_ids_are_checked_before_narrowing():
     with pytest.raises(ValueError):
         m.score_rows(torch.from_numpy(X))
     assert m.score_rows(np.array([[0, 10, 60, 61, 5]], dtype=np.int64)).shape == (1, 1)
+
+
+def test_dfm_projection_auto_plan():
+    """ABI v3 planning: AUTO plans P for the fp32 MLP exactly when rows >= 2 x
+    table rows (the projected workspace is what ON reports) and never for the
+    bf16 MLP; ON plans it for both."""
+    from hhfm_amd._native import native
+    nat = native()
+    dims = [400, 400, 400]
+    for md in (0, 1):
+        off = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 0)
+        on = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 1)
+        assert on - off >= 5 * 5051 * 416 * 4
+        auto = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 2)
+        assert auto == (on if md == 0 else off)
+        small = nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 2)
+        assert small == nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 0)
+        assert off == nat.dfm_forward_workspace(1 << 20, dims, md)
+    # outside the fused envelope (k % 16 != 0) nothing is planned
+    assert (nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 1)
+            == nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 0))

@@ -107,8 +107,9 @@ def test_dfm_forward_shapes(mlp, k, layers):
         assert np.all(np.abs(got - ref) <= 5e-3 * mag)
 
 
+@pytest.mark.parametrize("proj", [False, True])
 @pytest.mark.parametrize("mlp", ["f32", "bf16"])
-def test_dfm_catalog_topk_chunked(mlp):
+def test_dfm_catalog_topk_chunked(mlp, proj):
     """Query chunking (chunk_rows < B*N) gives the same top-K as one pass
     (bf16: the fused kernel scores the chunks; oracle rounds like it)."""
     from hhfm_amd import ops
@@ -135,7 +136,7 @@ def test_dfm_catalog_topk_chunked(mlp):
     q = torch.from_numpy(A).cuda()
     for chunk in (1 << 20, 1000, 701):
         s, i = ops.dfm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,
-                                    dims, Wp, bp, 1, nu, ni, 20, 0, chunk)
+                                    dims, Wp, bp, 1, nu, ni, 20, 0, chunk, proj=proj)
         rs, ri = orc.top_k(sc, 20)
         tol = (1e-5 if mlp == "f32" else 5e-3) * np.abs(sc).max(1, keepdims=True)
         bad, swaps = orc.topk_swaps(sc, ri, i.cpu().numpy(), tol)
@@ -188,3 +189,49 @@ def test_dfm_fused_envelope(F, k, layers, tdt, B, mlp):
     else:
         ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
         assert np.all(np.abs(got - ref) <= 2e-5 * mag), np.max(np.abs(got - ref) / mag)
+
+
+@pytest.mark.parametrize("F,k,layers,tdt,B", [
+    (5, 256, [400, 400, 400], "f32", 3001),     # C5 shape (TM = 13)
+    (5, 64, [150, 200, 150], "bf16", 5000),     # the reference's layers
+    (5, 16, [33], "bf16", 129),                 # one layer: no hidden chunks
+    (3, 48, [64, 96, 33, 20], "f32", 1000),     # 4 layers, odd widths
+    (11, 32, [128, 416], "bf16", 1),            # widest envelope, one row
+])
+@pytest.mark.parametrize("mlp", ["bf16", "f32"])
+def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp):
+    """Projected layer 0 (h_0 = Σ_f P_f[x_f], dfm_fused.hip PROJ kernels),
+    forced on, against the same oracles and tolerances as the direct kernels,
+    and against the direct kernel itself (bf16: summation order only, so the
+    two differ by at most a bf16 flip of a hidden unit)."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(F * 7919 + k)
+    M = 997
+    tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
+    mdt = torch.bfloat16 if mlp == "bf16" else torch.float32
+    m = _model((100, 200, M, F, k, layers), mlp_dtype=mdt, table_dtype=tdtype)
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    W = m.get_weights()
+    L = len(layers)
+    Ls = [W[f"layer_{i}"] for i in range(L)]
+    Bs = [W[f"bias_{i}"] for i in range(L)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    if tdt == "bf16":
+        E = bf16_round(E)
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    Wt, bs, dims, Wpd, bpd = m._prepared()
+    xd = torch.from_numpy(X).cuda()
+    wb = m.weights["feature_bias"].reshape(-1)
+    got = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, mdt, Wpd, bpd, proj=True).cpu().numpy()
+    direct = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, mdt, Wpd, bpd,
+                             proj=False).cpu().numpy()
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    if mlp == "bf16":
+        ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+        tol = 5e-3
+    else:
+        ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
+        tol = 2e-5
+    assert np.all(np.abs(got - ref) <= tol * mag), np.max(np.abs(got - ref) / mag)
+    assert np.all(np.abs(got - direct) <= tol * mag), np.max(np.abs(got - direct) / mag)
+
