@@ -386,10 +386,14 @@ def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
             "checksum_note": "catalog seeded by global item index: identical for every N"}
 
 
-def c5_leg(dev, world, rank, rows, reps=3):
-    """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137) on the
-    fused bf16-MFMA kernel, Frappe vocabulary, `rows` rows per GPU (12.5M =
-    the 100M-row job over 8 GPUs; weak scaling, rows sharded, no collective)."""
+def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
+    """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137),
+    Frappe vocabulary, `rows` rows per GPU (12.5M = the 100M-row job over 8
+    GPUs; weak scaling, rows sharded, no collective).  mlp=bf16: the fused
+    bf16-MFMA kernel (direct layer 0); mlp=fp32 (the reference numerics):
+    exact-fp32 MFMA with the projected layer 0 (include/hhfm.h ABI v3: P =
+    W0-projection of every table row once per call inside the timed step,
+    h0 = Σ_f P_f[x_f]) — its roofline counts the FLOPs it executes."""
     from hhfm_amd import ops
     from hhfm_amd.DFM import DeepFM
     nu, ni, ctx = 957, 4082, (7, 2, 3)
@@ -405,13 +409,13 @@ def c5_leg(dev, world, rank, rows, reps=3):
     X = torch.stack(cols, 1).to(torch.int32).contiguous()
     del cols
     m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
-               mlp_dtype=torch.bfloat16)
+               mlp_dtype=mlp)
     Wt, bs, dims, Wp, bp = m._prepared()
     out = torch.empty(rows, device=dev)
     wb = m.weights["feature_bias"].reshape(-1)
 
     def step():
-        ops.dfm_forward(X, m.table, wb, Wt, bs, dims, torch.bfloat16, Wp, bp, out=out)
+        ops.dfm_forward(X, m.table, wb, Wt, bs, dims, mlp, Wp, bp, out=out)
 
     step()
     torch.cuda.synchronize()
@@ -434,14 +438,28 @@ def c5_leg(dev, world, rank, rows, reps=3):
     ms = float(t[0]) / reps * 1e3
     kern = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     fl = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
-    return {"workload": "C5 (configs[4]): DeepFM F=5 k=256 + MLP 3x400 (bf16 MFMA, fp32 "
-                        "table and accumulation), Frappe vocabulary, rows sharded "
-                        f"{rows:,} per GPU", "ranks": world,
-            "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
-            "roofline": {"bound": "mfma", "flops_per_row": fl,
-                         "achieved_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
-                         "peak_TFLOPs": 2500.0,
-                         "frac": fl * rows / (kern * 1e-3) / 1e12 / 2500.0}}
+    if mlp == torch.bfloat16:
+        return {"workload": "C5 (configs[4]): DeepFM F=5 k=256 + MLP 3x400 (bf16 MFMA, fp32 "
+                            "table and accumulation), Frappe vocabulary, rows sharded "
+                            f"{rows:,} per GPU", "ranks": world,
+                "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
+                "roofline": {"bound": "mfma", "flops_per_row": fl,
+                             "achieved_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
+                             "peak_TFLOPs": 2500.0,
+                             "frac": fl * rows / (kern * 1e-3) / 1e12 / 2500.0}}
+    # executed FLOPs of the projected path: the per-call projection of the
+    # M table rows (5 GEMMs [M,256]x[256,400]) + the hidden layers per row
+    ex = 2.0 * 5 * M * 256 * 400 + rows * (2.0 * 2 * 400 * 400 + 2.0 * (5 * 416 + 256 + 400))
+    return {"workload": "C5 (configs[4]) at the reference numerics: DeepFM F=5 k=256 + MLP "
+                        "3x400, exact-fp32 MFMA, projected layer 0 (P computed inside every "
+                        f"step), Frappe vocabulary, rows sharded {rows:,} per GPU",
+            "ranks": world, "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms,
+            "kernel_ms": kern,
+            "reference_flops_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
+            "roofline": {"bound": "mfma", "executed_flops_per_pass": ex,
+                         "achieved_TFLOPs": ex / (kern * 1e-3) / 1e12,
+                         "peak_TFLOPs": 157.3,
+                         "frac": ex / (kern * 1e-3) / 1e12 / 157.3}}
 
 
 def stream_read_peak(buf, reps=5):
@@ -606,6 +624,11 @@ def main():
             extra["dfm_c5"] = c5_leg(dev, world, rank, args.c5_rows)
         except Exception as e:  # noqa: BLE001
             extra["dfm_c5"] = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+        try:
+            extra["dfm_c5_f32"] = c5_leg(dev, world, rank, args.c5_rows, mlp=torch.float32)
+        except Exception as e:  # noqa: BLE001
+            extra["dfm_c5_f32"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
     if "hr" in legs and rank == 0:
         try:

@@ -34,8 +34,10 @@
 // row m's input is the concat of F table rows, so
 //   h_0[m] = Σ_f W0[:, f·k:(f+1)·k] · E[x_f]  =  Σ_f P_f[x_f]
 // with P_f[id] = W0_f · E[id] computed ONCE per call for every table row
-// (dfm_project_layer0: F MFMA GEMMs [M, k] x [k, N0], the same bf16-rounded
-// operands / exact-fp32 products as the direct kernel, fp32 results).  When
+// (dfm_project_layer0: F MFMA GEMMs [M, k] x [k, N0] over the same operands
+// as the direct kernel — bf16-rounded for the bf16 MLP, exact fp32 for the
+// fp32 MLP — fp32 results; a bf16 P was measured: 7 % faster, and its extra
+// rounding moved bf16-MLP catalog rankings past the 5e-3 test bound).  When
 // the rows outnumber the table rows (rows >= 2·M; C5 scores 12.5 M rows
 // against 5,051 table rows) this removes layer 0's MFMA work (61 % of C5's
 // FLOPs) and its weight stream: the kernel gathers F rows of P per row
@@ -71,9 +73,12 @@ struct FusedDfmArgs {
   float bp;
   float* out;
   const uint4* packed;   // chunk sequence written by dfm_pack_weights
-  const float* proj;     // PROJ: P_f[id][n] at proj + f·proj_fstride + id·proj_ld + n
+  // PROJ: fp32 P_f[id] at proj + f·proj_fstride + id·proj_ld, zero beyond
+  // dims[0]; fp32 MLP: natural unit order; bf16 MLP: the accumulator order of
+  // dfm_proj_pos (a lane's 16 units of a tile are contiguous)
+  const void* proj;
   int64_t proj_fstride;
-  int proj_ld;           // 32·TM (zero beyond dims[0])
+  int proj_ld;           // 32·TM
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -248,25 +253,32 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     // ----- projected layer 0: acc = Σ_f P_f[x_f], FM part from the table -----
     if (nchunks > 0) dma(0, 0);   // first hidden chunk streams behind the gathers
     // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
-    // one float4 of P per (field, tile, g); all 4·TM of a field in flight
+    // one float4 of P per (field, tile, g); all 4·TM of a field in flight.
+    // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
+    // HHFM_KO_PROJFM skip the P / FM loads — scripts/build_variants.sh.)
+#ifndef HHFM_KO_PROJP
     for (int f = 0; f < F; ++f) {
+      // P in accumulator order: positions 32t + 16h .. +15 are this lane's
+      // units of tile t (64 contiguous bytes)
       const float4* pp = reinterpret_cast<const float4*>(
-                             a.proj + f * a.proj_fstride +
-                             (int64_t)ids[myrow * F + f] * a.proj_ld) + h;
+                             reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
+                             (int64_t)ids[myrow * F + f] * a.proj_ld) + 4 * h;
 #pragma unroll
       for (int t = 0; t < TM; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 x = pp[8 * t + 2 * g4];
+          const float4 x = pp[8 * t + g4];
           acc[t][4 * g4 + 0] += x.x;
           acc[t][4 * g4 + 1] += x.y;
           acc[t][4 * g4 + 2] += x.z;
           acc[t][4 * g4 + 3] += x.w;
         }
     }
+#endif
     // FM second-order part (DFM.py:114-122): the lane half h takes columns
     // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
     for (int j = 0; j < k / 16; ++j) {
+#ifndef HHFM_KO_PROJFM
       float s8[8], q8[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) { s8[q] = 0.f; q8[q] = 0.f; }
@@ -302,6 +314,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) d += 0.5f * (s8[q] * s8[q] - q8[q]) * wq[q];
       y2 += d;
+#endif
     }
     __syncthreads();   // vmcnt(0): hidden chunk 0 landed
   } else {
@@ -607,7 +620,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
     if (nchunks > 0) dma(0, 0);
     for (int f = 0; f < F; ++f) {
       const float4* pp = reinterpret_cast<const float4*>(
-                             a.proj + f * a.proj_fstride +
+                             reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
                              (int64_t)ids[myrow * F + f] * a.proj_ld) + kq;
 #pragma unroll
       for (int t = 0; t < T16; ++t) {
@@ -785,7 +798,8 @@ bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims) {
 
 int dfm_proj_ld(int L, const int32_t* dims) { return 32 * fused_tm(fused_max_tiles(L, dims)); }
 
-size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims) {
+size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims, bool mlp_bf16) {
+  (void)mlp_bf16;   // P is fp32 for both MLP dtypes
   const size_t p = (size_t)F * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
   return ((p + 255) & ~size_t(255)) + (((size_t)M * 4 + 255) & ~size_t(255));
 }
@@ -794,13 +808,12 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
                         const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
                         hipStream_t st) {
   const int ld = dfm_proj_ld(L, dims);
+  const size_t esz = mlp_bf16 ? 2 : 4;   // weight element size
   const size_t pbytes = ((size_t)F * M * ld * 4 + 255) & ~size_t(255);
-  float* P = reinterpret_cast<float*>(ws);
   int32_t* iota = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + pbytes);
   const int64_t ib = (M + 255) / 256 < 4096 ? (M + 255) / 256 : 4096;
   hipLaunchKernelGGL(dfm_iota, dim3((unsigned)ib), dim3(256), 0, st, iota, M);
   const int ldb0 = (F * k + 7) & ~7;
-  const size_t esz = mlp_bf16 ? 2 : 4;
   for (int f = 0; f < F; ++f) {
     GemmArgs g{};
     g.M = M;
@@ -810,8 +823,9 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
     g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)f * k * esz;
     g.ldb = ldb0;
     g.relu = 0;
-    g.C = P + (size_t)f * M * ld;
+    g.C = reinterpret_cast<float*>(ws) + (size_t)f * M * ld;
     g.ldc = ld;
+    g.c_perm32 = mlp_bf16;   // the bf16 kernel's accumulator order
     launch_gemm(g, mlp_bf16, 0, st);
   }
 }
@@ -821,7 +835,7 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, const float* proj, hipStream_t st) {
+                      float* out, void* pack_ws, const void* proj, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -854,11 +868,11 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
 #define HHFM_FUSED32(T)                                                                    \
   case T:                                                                                  \
     if (pj) {                                                                              \
-      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, true>), grid, dim3(256), 0, st, a);  \
-      else hipLaunchKernelGGL((dfm_fused_f32<false, T, true>), grid, dim3(256), 0, st, a);     \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, true>), grid, dim3(256), 0, st, a); \
+      else hipLaunchKernelGGL((dfm_fused_f32<false, T, true>), grid, dim3(256), 0, st, a);    \
     } else {                                                                               \
-      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, false>), grid, dim3(256), 0, st, a); \
-      else hipLaunchKernelGGL((dfm_fused_f32<false, T, false>), grid, dim3(256), 0, st, a);    \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32<true, T, false>), grid, dim3(256), 0, st, a);\
+      else hipLaunchKernelGGL((dfm_fused_f32<false, T, false>), grid, dim3(256), 0, st, a);   \
     }                                                                                      \
     break;
     switch (TM) {
@@ -884,11 +898,11 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
 #define HHFM_FUSED(T)                                                                      \
   case T:                                                                                  \
     if (pj) {                                                                              \
-      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, true>), grid, dim3(256), 0, st, a);      \
-      else hipLaunchKernelGGL((dfm_fused<false, T, true>), grid, dim3(256), 0, st, a);         \
+      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, true>), grid, dim3(256), 0, st, a);     \
+      else hipLaunchKernelGGL((dfm_fused<false, T, true>), grid, dim3(256), 0, st, a);        \
     } else {                                                                               \
-      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, false>), grid, dim3(256), 0, st, a);     \
-      else hipLaunchKernelGGL((dfm_fused<false, T, false>), grid, dim3(256), 0, st, a);        \
+      if (tbf) hipLaunchKernelGGL((dfm_fused<true, T, false>), grid, dim3(256), 0, st, a);    \
+      else hipLaunchKernelGGL((dfm_fused<false, T, false>), grid, dim3(256), 0, st, a);       \
     }                                                                                      \
     break;
   switch (TM) {

@@ -44,6 +44,14 @@ HHFM_DEV void split3x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) 
 
 constexpr int GBM = 128, GBN = 128;
 
+// Column order of the projected layer 0 for the bf16 fused DeepFM kernel
+// (dfm_fused.hip): unit n = 32t + 8g + 4h + e of a 32x32x16 result tile sits
+// in lane half h, register 4g + e, so storing it at 32t + 16h + 4g + e makes
+// each lane's 16 units of a tile contiguous.
+HHFM_DEV int dfm_proj_pos(int n) {
+  return (n & ~31) | (((n >> 2) & 1) << 4) | (((n >> 3) & 3) << 2) | (n & 3);
+}
+
 struct GemmArgs {
   int64_t M;
   int N, K;
@@ -70,6 +78,7 @@ struct GemmArgs {
   int G;                // grouped dot: group size (16, 32 or 64)
   int mod;              // grouped dot: bias / v are indexed by n % mod
   int64_t ldp;          // grouped dot: row stride of partial
+  int c_perm32;         // epilogue 0: column n stored at dfm_proj_pos(n)
   int ksplit;           // split-K (epilogue 0): blockIdx.z covers K range
                         // [z*ksplit, (z+1)*ksplit), ksplit % 32 == 0, and
   int64_t cz_stride;    // stores to C + z*cz_stride (elements); 0 = no split
@@ -270,10 +279,11 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
             if (g.rowbias) v += g.rowbias[m];
             if (g.relu) v = fmaxf(v, 0.f);
             if (n >= g.N) v = 0.f;  // zero pad columns: next layer's K padding
+            const int nn = g.c_perm32 ? dfm_proj_pos(n) : n;
             if (g.c_bf16)
-              reinterpret_cast<uint16_t*>(g.C)[cz + m * g.ldc + n] = f2bf(v);
+              reinterpret_cast<uint16_t*>(g.C)[cz + m * g.ldc + nn] = f2bf(v);
             else
-              reinterpret_cast<float*>(g.C)[cz + m * g.ldc + n] = v;
+              reinterpret_cast<float*>(g.C)[cz + m * g.ldc + nn] = v;
           }
         }
     }

@@ -29,9 +29,9 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, const float* proj, hipStream_t st);
+                      float* out, void* pack_ws, const void* proj, hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
-size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims);
+size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims, bool mlp_bf16);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
                         const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
                         hipStream_t st);
@@ -142,7 +142,7 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   p.off_proj = off;
   if (proj_mode != HHFM_DFM_PROJ_OFF && M > 0 && dfm_proj_eligible(F, k, nlayers, dims) &&
       (proj_mode == HHFM_DFM_PROJ_ON || (mlp_dtype == HHFM_F32 && rows_total >= 2 * M))) {
-    const size_t pb = dfm_proj_bytes(F, M, nlayers, dims);
+    const size_t pb = dfm_proj_bytes(F, M, nlayers, dims, mlp_dtype == HHFM_BF16);
     if (pb <= kProjMaxBytes) {
       p.proj = true;
       off += al256(pb);
@@ -170,7 +170,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             int64_t M, int32_t k, int32_t dtype, const float* w,
                             int32_t nlayers, const int32_t* dims, const void* const* Wt,
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
-                            float bp, float* out, char* ws, const DfmPlan& p, const float* proj,
+                            float bp, float* out, char* ws, const DfmPlan& p, const void* proj,
                             hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
   // One fused kernel per 128-row block when the shape fits (dfm_fused.hip,
@@ -269,11 +269,11 @@ extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const 
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const float* proj = nullptr;
+  const void* proj = nullptr;
   if (p.proj) {
     dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
                        layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
-    proj = reinterpret_cast<const float*>(ws + p.off_proj);
+    proj = ws + p.off_proj;
   }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
                           mlp_dtype, Wp, bp, out, ws, p, proj, st);
@@ -350,11 +350,11 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   int32_t* rbuf = reinterpret_cast<int32_t*>(ws + p.total);
   float* sc = reinterpret_cast<float*>(ws + p.total + al256((size_t)rows * F * 4));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const float* proj = nullptr;
+  const void* proj = nullptr;
   if (p.proj) {   // once per call: every query chunk reuses it
     dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
                        layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
-    proj = reinterpret_cast<const float*>(ws + p.off_proj);
+    proj = ws + p.off_proj;
   }
   for (int64_t b0 = 0; b0 < B; b0 += qc) {
     const int64_t nb = (B - b0) < qc ? (B - b0) : qc;

@@ -178,7 +178,8 @@ int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_
 /* Projected layer 0 (ABI v3).  Layer 0 is linear before its ReLU, so
  * h_0 = Σ_f P_f[x_f] with P_f[id] = W0[:, f·k:(f+1)·k] · E[id]: the forward
  * computes P for every table row and field once per call (F MFMA GEMMs, the
- * direct kernel's operand rounding) and the fused kernel gathers it instead
+ * direct kernel's operand rounding, fp32 results) and the fused kernel
+ * gathers it instead
  * of streaming layer 0's weights — a saving when rows >= 2·features_M
  * (DFM.py:125-128 computed by the same products, summed per field first).
  * hhfm_dfm_forward / hhfm_dfm_catalog_topk take that path when ws_bytes

@@ -170,7 +170,7 @@ def test_dfm_projection_auto_plan():
     for md in (0, 1):
         off = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 0)
         on = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 1)
-        assert on - off >= 5 * 5051 * 416 * 4
+        assert on - off >= 5 * 5051 * 416 * 4   # fp32 P
         auto = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 2)
         assert auto == (on if md == 0 else off)
         small = nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 2)
