@@ -487,6 +487,29 @@ def stream_read_peak(buf, reps=5):
     return max(rates.values()), rates
 
 
+def gather_rows_peak(idx, E, reps=5):
+    """The box's measured ceiling for K1's access pattern: the same row
+    kernel over the same user and item columns (two random 256-B table rows
+    per row) with the `w` and context loads removed (F=2, w=None), best of
+    `reps` launches -> GB/s of its bytes (2 rows + 2 ids + out per row)."""
+    from hhfm_amd import ops
+    ui = idx[:, :2].contiguous()
+    o = torch.empty(ui.shape[0], dtype=torch.float32, device=idx.device)
+    ops.fm_score_rows(ui, E, None, 0.0, out=o)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        ops.fm_score_rows(ui, E, None, 0.0, out=o)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    bpr = 2 * E.shape[1] * E.element_size() + 2 * 4 + 4
+    del ui, o
+    return bpr * idx.shape[0] / (best * 1e-3) / 1e9, best
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -550,6 +573,7 @@ def main():
     # + ids + out = 792 B/row at k=64.
     bpr_lines = 2 * args.k * 4 + 2 * 128 + 5 * 4 + 4
     peak_meas, peak_variants = stream_read_peak(E)
+    gather_peak, gather_ms = gather_rows_peak(idx, E)
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -587,6 +611,11 @@ def main():
                                           "4.3 GB table, best variant and launch of 5, this box",
                      "peak_measured_variants": peak_variants,
                      "frac_vs_measured": (achieved / peak_meas) if peak_meas else None,
+                     "peak_gather_measured": gather_peak,
+                     "peak_gather_how": "the same row kernel over the same rows' user and item "
+                                        "columns only (2 random 256-B rows, no w / context "
+                                        f"loads): {gather_ms:.3f} ms, best of 5, this box",
+                     "frac_vs_gather": achieved / gather_peak,
                      "line_bytes_per_row": bpr_lines,
                      "line_rate_GBps": bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9,
                      "line_frac_vs_measured": (bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9
