@@ -58,3 +58,5 @@ def test_stream_read_probe_and_c5_leg_run():
     assert 500 < gbs < 20000 and len(var) == 3, (gbs, var)
     r = bench.c5_leg(dev, 1, 0, 100_000, reps=1)
     assert np.isfinite(r["rows_per_s"]) and r["roofline"]["frac"] > 0
+    r = bench.c5_leg(dev, 1, 0, 100_000, reps=1, mlp=torch.float32)   # projected layer 0
+    assert np.isfinite(r["rows_per_s"]) and 0 < r["roofline"]["frac"] < 1
