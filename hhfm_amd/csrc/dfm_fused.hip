@@ -79,6 +79,8 @@ struct FusedDfmArgs {
   const void* proj;
   int64_t proj_fstride;
   int proj_ld;           // 32·TM
+  int Fd;                // fields [0, Fd) run layer 0 on MFMA, [Fd, F) come from P
+                         // (Fd = F: no projection; 0: all fields projected)
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -100,7 +102,8 @@ HHFM_DEV void swap_halves(uint32_t& a, uint32_t& b) {
 __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, int nc0, int NC,
                                                         uint4* __restrict__ out) {
   const int NR = 32 * TM;
-  const int nS = a.F * (a.k / 16);
+  const int Fd = a.Fd;                        // layer-0 K covers the direct fields only
+  const int nS = Fd * (a.k / 16);
   const int64_t total = (int64_t)(nc0 + (a.L - 1) * NC) * NR * 8;
   for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
        x += (int64_t)gridDim.x * blockDim.x) {
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, 
       i = 0;
       const int S = 4 * g + (u >> 1);
       ok = S < nS;
-      kk = (S % a.F) * a.k + 16 * (S / a.F) + 8 * (u & 1);
+      kk = (S % Fd) * a.k + 16 * (S / Fd) + 8 * (u & 1);
     } else {
       i = 1 + (g - nc0) / NC;
       kk = 64 * ((g - nc0) % NC) + 8 * u;
@@ -145,8 +148,10 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   const int r = l & 31, h = l >> 5;
   const int64_t m0 = (int64_t)blockIdx.x * kFusedRows;
   const int F = a.F, k = a.k, L = a.L;
-  const int nS = F * (k / 16);               // layer-0 k16 steps
-  const int nc0 = PROJ ? 0 : (nS + 3) / 4;   // layer-0 K-chunks (none when projected)
+  // layer 0 on MFMA over the direct fields [0, Fd); fields [Fd, F) come from P
+  const int Fd = PROJ ? a.Fd : F;
+  const int nS = Fd * (k / 16);              // layer-0 k16 steps
+  const int nc0 = (nS + 3) / 4;              // layer-0 K-chunks (none when all projected)
   const int nchunks = nc0 + (L - 1) * NC;
 
   for (int x = tid; x < kFusedRows * F; x += 256) {
@@ -189,7 +194,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   };
   auto adv = [&](Cur& u) {
     ++u.S;
-    if (++u.f == F) {
+    if (++u.f == Fd) {
       u.f = 0;
       u.col += 16;
     }
@@ -250,18 +255,20 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   };
 
   if constexpr (PROJ) {
-    // ----- projected layer 0: acc = Σ_f P_f[x_f], FM part from the table -----
-    if (nchunks > 0) dma(0, 0);   // first hidden chunk streams behind the gathers
+    // ----- projected layer 0: acc = Σ_{f >= Fd} P_f[x_f]; with Fd == 0 also
+    // the FM part from the table (otherwise the direct loop below adds the
+    // MFMA part of fields < Fd and the FM part) -----
+    if (Fd == 0 && nchunks > 0) dma(0, 0);   // hidden chunk 0 streams behind the gathers
     // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
     // one float4 of P per (field, tile, g); all 4·TM of a field in flight.
     // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
     // HHFM_KO_PROJFM skip the P / FM loads — scripts/build_variants.sh.)
 #ifndef HHFM_KO_PROJP
-    for (int f = 0; f < F; ++f) {
+    for (int f = Fd; f < F; ++f) {
       // P in accumulator order: positions 32t + 16h .. +15 are this lane's
       // units of tile t (64 contiguous bytes)
       const float4* pp = reinterpret_cast<const float4*>(
-                             reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
+                             reinterpret_cast<const float*>(a.proj) + (f - Fd) * a.proj_fstride +
                              (int64_t)ids[myrow * F + f] * a.proj_ld) + 4 * h;
 #pragma unroll
       for (int t = 0; t < TM; ++t)
@@ -277,7 +284,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 #endif
     // FM second-order part (DFM.py:114-122): the lane half h takes columns
     // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
-    for (int j = 0; j < k / 16; ++j) {
+    for (int j = 0; j < (Fd == 0 ? k / 16 : 0); ++j) {
 #ifndef HHFM_KO_PROJFM
       float s8[8], q8[8];
 #pragma unroll
@@ -316,8 +323,9 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
       y2 += d;
 #endif
     }
-    __syncthreads();   // vmcnt(0): hidden chunk 0 landed
-  } else {
+    if (Fd == 0) __syncthreads();   // vmcnt(0): hidden chunk 0 landed
+  }
+  if (!PROJ || Fd > 0) {
   EChunk e0, e1;
   Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
   eload(e0, cg);
@@ -375,7 +383,36 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         fs[q] += v[j][q];
         fq[q] += v[j][q] * v[j][q];
       }
-      if (f == F - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
+      if (f == Fd - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
+        if constexpr (PROJ) {
+          // the projected fields' values of these 8 columns (their rows are
+          // few and cache-resident: Frappe's contexts)
+          for (int f2 = Fd; f2 < F; ++f2) {
+            const int64_t id2 = ids[myrow * F + f2];
+            float u8[8];
+            if constexpr (TBF) {
+              const uint4 x = *reinterpret_cast<const uint4*>(
+                  reinterpret_cast<const uint16_t*>(a.E) + id2 * k + cs.col + 8 * h);
+              const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+              for (int qq = 0; qq < 4; ++qq) {
+                u8[2 * qq] = __uint_as_float(x4[qq] << 16);
+                u8[2 * qq + 1] = __uint_as_float(x4[qq] & 0xffff0000u);
+              }
+            } else {
+              const float4* p2 = reinterpret_cast<const float4*>(
+                  reinterpret_cast<const float*>(a.E) + id2 * k + cs.col + 8 * h);
+              const float4 p0 = p2[0], p1 = p2[1];
+              u8[0] = p0.x; u8[1] = p0.y; u8[2] = p0.z; u8[3] = p0.w;
+              u8[4] = p1.x; u8[5] = p1.y; u8[6] = p1.z; u8[7] = p1.w;
+            }
+#pragma unroll
+            for (int qq = 0; qq < 8; ++qq) {
+              fs[qq] += u8[qq];
+              fq[qq] += u8[qq] * u8[qq];
+            }
+          }
+        }
         const float4* wc =
             reinterpret_cast<const float4*>(wpl + kFusedMaxF + cs.col + 8 * h);
         const float4 w0 = wc[0], w1 = wc[1];
@@ -798,23 +835,23 @@ bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims) {
 
 int dfm_proj_ld(int L, const int32_t* dims) { return 32 * fused_tm(fused_max_tiles(L, dims)); }
 
-size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims, bool mlp_bf16) {
-  (void)mlp_bf16;   // P is fp32 for both MLP dtypes
-  const size_t p = (size_t)F * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
+// P for the projected fields [proj_from, F)
+size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims) {
+  const size_t p = (size_t)(F - proj_from) * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
   return ((p + 255) & ~size_t(255)) + (((size_t)M * 4 + 255) & ~size_t(255));
 }
 
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
-                        const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
-                        hipStream_t st) {
+                        int proj_from, const void* Wt0, int N0, int L, const int32_t* dims,
+                        void* ws, hipStream_t st) {
   const int ld = dfm_proj_ld(L, dims);
   const size_t esz = mlp_bf16 ? 2 : 4;   // weight element size
-  const size_t pbytes = ((size_t)F * M * ld * 4 + 255) & ~size_t(255);
+  const size_t pbytes = ((size_t)(F - proj_from) * M * ld * 4 + 255) & ~size_t(255);
   int32_t* iota = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + pbytes);
   const int64_t ib = (M + 255) / 256 < 4096 ? (M + 255) / 256 : 4096;
   hipLaunchKernelGGL(dfm_iota, dim3((unsigned)ib), dim3(256), 0, st, iota, M);
   const int ldb0 = (F * k + 7) & ~7;
-  for (int f = 0; f < F; ++f) {
+  for (int f = proj_from; f < F; ++f) {
     GemmArgs g{};
     g.M = M;
     g.N = N0;
@@ -823,7 +860,7 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
     g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)f * k * esz;
     g.ldb = ldb0;
     g.relu = 0;
-    g.C = reinterpret_cast<float*>(ws) + (size_t)f * M * ld;
+    g.C = reinterpret_cast<float*>(ws) + (size_t)(f - proj_from) * M * ld;
     g.ldc = ld;
     g.c_perm32 = mlp_bf16;   // the bf16 kernel's accumulator order
     launch_gemm(g, mlp_bf16, 0, st);
@@ -831,11 +868,14 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
 }
 
 // returns false when the shape is outside the fused kernel's envelope.
-// proj != nullptr: layer 0 from dfm_project_layer0's workspace (PROJ kernels).
+// proj != nullptr: the layer-0 products of fields [proj_from, F) come from
+// dfm_project_layer0's workspace (PROJ kernels; the fp32 MLP projects all
+// fields, proj_from = 0).
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, const void* proj, hipStream_t st) {
+                      float* out, void* pack_ws, const void* proj, int proj_from,
+                      hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -857,7 +897,10 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.proj_ld = 32 * TM;
   a.proj_fstride = (int64_t)M * a.proj_ld;
   const bool pj = proj != nullptr;
+  a.Fd = pj ? proj_from : F;
+  if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
+    if (pj && proj_from != 0) return false;   // the fp32 kernel projects all fields
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
     const int nc0 = pj ? 0 : (F * (k / 16) + 1) / 2;
     const int64_t units = (int64_t)(nc0 + (L - 1) * TM) * 32 * TM * 8;
@@ -889,7 +932,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     return true;
   }
   const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
-  const int nS = F * (k / 16), nc0 = pj ? 0 : (nS + 3) / 4, NC = (TM + 1) / 2;
+  const int nS = a.Fd * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;
   const int64_t units = (int64_t)(nc0 + (L - 1) * NC) * 32 * TM * 8;
   const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
   if (units > 0)

@@ -29,12 +29,13 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
-                      float* out, void* pack_ws, const void* proj, hipStream_t st);
+                      float* out, void* pack_ws, const void* proj, int proj_from,
+                      hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
-size_t dfm_proj_bytes(int F, int64_t M, int L, const int32_t* dims, bool mlp_bf16);
+size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
-                        const void* Wt0, int N0, int L, const int32_t* dims, void* ws,
-                        hipStream_t st);
+                        int proj_from, const void* Wt0, int N0, int L, const int32_t* dims,
+                        void* ws, hipStream_t st);
 
 // ---------------------------------------------------------------------------
 // FM part of DeepFM and the final reduce
@@ -106,6 +107,7 @@ struct DfmPlan {
   size_t off_base, off_part, off_h0, off_h1, off_pack, off_proj, total;
   int maxL, ntl;
   bool proj;
+  int proj_from;   // first projected field (fields [proj_from, F) come from P)
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -115,14 +117,17 @@ static int pad8(int x) { return (x + 7) & ~7; }
 // Projected layer 0 (dfm_fused.hip): at most this much workspace for P.
 constexpr size_t kProjMaxBytes = size_t(1) << 30;
 
-// proj_mode: HHFM_DFM_PROJ_OFF plans no projection (F, k, M unused);
-// HHFM_DFM_PROJ_ON plans it whenever the fused kernels admit the shape and P
-// fits kProjMaxBytes; HHFM_DFM_PROJ_AUTO additionally needs the fp32 MLP and
-// rows_total >= 2·M (P costs one layer-0 row per table row and field).  With
-// the bf16 MLP the P gather (F·32·TM fp32 per row, table-row-random) costs
-// what the bf16 layer-0 MFMAs it removes cost — C5: 4.75 ms projected vs
-// 4.72 direct per 2 M rows — so AUTO leaves it direct; with the fp32 MLP
-// (16x slower MFMA) it halves C5 (17.2 vs 35.2 ms).
+// proj_mode (include/hhfm.h hhfm_dfm_proj): OFF plans no projection (F, k,
+// M unused); ON projects every field, CTX the fields >= 2 (LoadData's
+// contexts after user and item; bf16 MLP only) whenever the fused kernels
+// admit the shape and P fits kProjMaxBytes; AUTO picks ON for the fp32 MLP
+// when rows_total >= 2·M (P costs one layer-0 row per table row and field)
+// and CTX for the bf16 MLP under the same condition with F >= 3.  With the
+// bf16 MLP projecting every field is not a win — the user and item rows of P
+// are table-random fp32 rows, more bytes per row than the weight stream they
+// replace (C5 L3, bf16 table: 4.83 ms projected vs 4.51 direct per 2 M rows)
+// — while the context fields' P rows are few and cache-resident (CTX: 3.98
+// ms, -12 %; with an fp32 table +1.6 %, profiles/r02_dfm_ctx_phases.json).
 static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype, int F = 0,
                         int k = 0, int64_t M = 0, int64_t rows_total = 0,
                         int proj_mode = HHFM_DFM_PROJ_OFF) {
@@ -140,16 +145,30 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   if (dfm_fused_eligible(nlayers, dims))
     off += al256(dfm_fused_pack_bytes(nlayers, dims, mlp_dtype == HHFM_BF16));
   p.off_proj = off;
-  if (proj_mode != HHFM_DFM_PROJ_OFF && M > 0 && dfm_proj_eligible(F, k, nlayers, dims) &&
-      (proj_mode == HHFM_DFM_PROJ_ON || (mlp_dtype == HHFM_F32 && rows_total >= 2 * M))) {
-    const size_t pb = dfm_proj_bytes(F, M, nlayers, dims, mlp_dtype == HHFM_BF16);
+  p.proj_from = -1;
+  int mode = proj_mode;
+  if (mode == HHFM_DFM_PROJ_AUTO)
+    mode = rows_total < 2 * M ? HHFM_DFM_PROJ_OFF
+           : mlp_dtype == HHFM_F32 ? HHFM_DFM_PROJ_ON
+           : HHFM_DFM_PROJ_CTX;
+  int from = -1;
+  if (mode == HHFM_DFM_PROJ_ON) from = 0;
+  if (mode == HHFM_DFM_PROJ_CTX && mlp_dtype == HHFM_BF16 && F >= 3) from = 2;
+  if (from >= 0 && M > 0 && dfm_proj_eligible(F, k, nlayers, dims)) {
+    const size_t pb = dfm_proj_bytes(F, from, M, nlayers, dims);
     if (pb <= kProjMaxBytes) {
       p.proj = true;
+      p.proj_from = from;
       off += al256(pb);
     }
   }
   p.total = off;
   return p;
+}
+
+static bool proj_mode_ok(int m) {
+  return m == HHFM_DFM_PROJ_OFF || m == HHFM_DFM_PROJ_ON || m == HHFM_DFM_PROJ_AUTO ||
+         m == HHFM_DFM_PROJ_CTX;
 }
 
 static int dfm_check(int64_t B, int32_t F, int32_t k, int32_t dtype, int32_t nlayers,
@@ -181,7 +200,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
   }();
   if ((proj || !layered) && p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
-                       Wp, bp, out, ws + p.off_pack, proj, st))
+                       Wp, bp, out, ws + p.off_pack, proj, p.proj_from, st))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);
@@ -243,11 +262,41 @@ extern "C" int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k,
                                              int32_t proj_mode, size_t* ws_bytes) {
   if (!ws_bytes || B < 0 || F < 1 || k < 1 || features_M < 1 || nlayers < 1 || !layer_dims)
     return HHFM_EINVAL;
-  if (proj_mode != HHFM_DFM_PROJ_OFF && proj_mode != HHFM_DFM_PROJ_ON &&
-      proj_mode != HHFM_DFM_PROJ_AUTO)
-    return HHFM_EINVAL;
+  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
   *ws_bytes = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode).total;
   return HHFM_OK;
+}
+
+static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                               int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                               int32_t nlayers, const int32_t* layer_dims,
+                               const void* const* Wt, const float* const* bias,
+                               int32_t mlp_dtype, const float* Wp, float bp, float* out,
+                               char* ws, const DfmPlan& p, hipStream_t st) {
+  const void* proj = nullptr;
+  if (p.proj) {
+    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F,
+                       p.proj_from, Wt[0], layer_dims[0], nlayers, layer_dims,
+                       ws + p.off_proj, st);
+    proj = ws + p.off_proj;
+  }
+  return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
+                          mlp_dtype, Wp, bp, out, ws, p, proj, st);
+}
+
+static int dfm_forward_args(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                            int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                            int32_t nlayers, const int32_t* layer_dims, const void* const* Wt,
+                            const float* const* bias, int32_t mlp_dtype, const float* Wp,
+                            float* out) {
+  int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
+  if (rc) return rc;
+  if (features_M < 1) return HHFM_EINVAL;
+  if (B == 0) return HHFM_OK;
+  if (!idx || !E || !w || !Wt || !bias || !Wp || !out) return HHFM_EINVAL;
+  for (int i = 0; i < nlayers; ++i)
+    if (!Wt[i] || !bias[i]) return HHFM_EINVAL;
+  return 1;   // proceed
 }
 
 extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
@@ -256,27 +305,34 @@ extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const 
                                 const void* const* Wt, const float* const* bias,
                                 int32_t mlp_dtype, const float* Wp, float bp, float* out,
                                 void* workspace, size_t ws_bytes, void* stream) {
-  int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
-  if (rc) return rc;
-  if (features_M < 1) return HHFM_EINVAL;
-  if (B == 0) return HHFM_OK;
-  if (!idx || !E || !w || !Wt || !bias || !Wp || !out) return HHFM_EINVAL;
-  for (int i = 0; i < nlayers; ++i)
-    if (!Wt[i] || !bias[i]) return HHFM_EINVAL;
-  // the projected layer 0 runs when the workspace holds its plan
+  const int rc = dfm_forward_args(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
+                                  bias, mlp_dtype, Wp, out);
+  if (rc != 1) return rc;
+  // v3 behaviour: every field projected when the workspace holds that plan
   DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, HHFM_DFM_PROJ_ON);
   if (!p.proj || !workspace || ws_bytes < p.total) p = dfm_plan(B, nlayers, layer_dims, mlp_dtype);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
-  char* ws = reinterpret_cast<char*>(workspace);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const void* proj = nullptr;
-  if (p.proj) {
-    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
-                       layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
-    proj = ws + p.off_proj;
-  }
-  return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
-                          mlp_dtype, Wp, bp, out, ws, p, proj, st);
+  return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
+                             bias, mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
+                             reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                                   int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                                   int32_t nlayers, const int32_t* layer_dims,
+                                   const void* const* Wt, const float* const* bias,
+                                   int32_t mlp_dtype, const float* Wp, float bp, float* out,
+                                   int32_t proj_mode, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
+  const int rc = dfm_forward_args(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
+                                  bias, mlp_dtype, Wp, out);
+  if (rc != 1) return rc;
+  const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode);
+  if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
+  return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
+                             bias, mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 // D2: chunk_rows bounds the rows (queries x items) scored per forward pass.
@@ -310,9 +366,7 @@ extern "C" int hhfm_dfm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t 
   if (!ws_bytes || B < 0 || F < 1 || k < 1 || features_M < 1 || item_count < 1 ||
       chunk_rows < 1 || nlayers < 1 || !layer_dims)
     return HHFM_EINVAL;
-  if (proj_mode != HHFM_DFM_PROJ_OFF && proj_mode != HHFM_DFM_PROJ_ON &&
-      proj_mode != HHFM_DFM_PROJ_AUTO)
-    return HHFM_EINVAL;
+  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
   const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
@@ -321,15 +375,14 @@ extern "C" int hhfm_dfm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t 
   return HHFM_OK;
 }
 
-extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
-                                     const void* E, int64_t features_M, int32_t k, int32_t dtype,
-                                     const float* w, int32_t nlayers, const int32_t* layer_dims,
-                                     const void* const* Wt, const float* const* bias,
-                                     int32_t mlp_dtype, const float* Wp, float bp,
-                                     int32_t item_row_begin, int32_t item_count,
-                                     int32_t global_item_base, int32_t K, int64_t chunk_rows,
-                                     float* top_score, int32_t* top_idx, void* workspace,
-                                     size_t ws_bytes, void* stream) {
+static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
+                           const void* E, int64_t features_M, int32_t k, int32_t dtype,
+                           const float* w, int32_t nlayers, const int32_t* layer_dims,
+                           const void* const* Wt, const float* const* bias, int32_t mlp_dtype,
+                           const float* Wp, float bp, int32_t item_row_begin,
+                           int32_t item_count, int32_t global_item_base, int32_t K,
+                           int64_t chunk_rows, float* top_score, int32_t* top_idx,
+                           void* workspace, size_t ws_bytes, int proj_mode, void* stream) {
   int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
   if (rc) return rc;
   if (item_col < 0 || item_col >= F || item_count < 1 || item_row_begin < 0 ||
@@ -341,10 +394,16 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   if (!qidx || !E || !w || !Wt || !bias || !Wp || !top_score || !top_idx) return HHFM_EINVAL;
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
-  DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                       B * (int64_t)item_count, HHFM_DFM_PROJ_ON);
-  if (!p.proj || !workspace || ws_bytes < dfm_cat_bytes(p, rows, F))
-    p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
+  DfmPlan p;
+  if (proj_mode < 0) {   // legacy entry point: every field projected when the workspace holds it
+    p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
+                 B * (int64_t)item_count, HHFM_DFM_PROJ_ON);
+    if (!p.proj || !workspace || ws_bytes < dfm_cat_bytes(p, rows, F))
+      p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
+  } else {
+    p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
+                 B * (int64_t)item_count, proj_mode);
+  }
   if (!workspace || ws_bytes < dfm_cat_bytes(p, rows, F)) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   int32_t* rbuf = reinterpret_cast<int32_t*>(ws + p.total);
@@ -352,8 +411,9 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const void* proj = nullptr;
   if (p.proj) {   // once per call: every query chunk reuses it
-    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F, Wt[0],
-                       layer_dims[0], nlayers, layer_dims, ws + p.off_proj, st);
+    dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F,
+                       p.proj_from, Wt[0], layer_dims[0], nlayers, layer_dims,
+                       ws + p.off_proj, st);
     proj = ws + p.off_proj;
   }
   for (int64_t b0 = 0; b0 < B; b0 += qc) {
@@ -370,6 +430,38 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
                       top_idx + b0 * K, st);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
+                                     const void* E, int64_t features_M, int32_t k, int32_t dtype,
+                                     const float* w, int32_t nlayers, const int32_t* layer_dims,
+                                     const void* const* Wt, const float* const* bias,
+                                     int32_t mlp_dtype, const float* Wp, float bp,
+                                     int32_t item_row_begin, int32_t item_count,
+                                     int32_t global_item_base, int32_t K, int64_t chunk_rows,
+                                     float* top_score, int32_t* top_idx, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+  return dfm_catalog_run(qidx, B, F, item_col, E, features_M, k, dtype, w, nlayers, layer_dims,
+                         Wt, bias, mlp_dtype, Wp, bp, item_row_begin, item_count,
+                         global_item_base, K, chunk_rows, top_score, top_idx, workspace,
+                         ws_bytes, -1, stream);
+}
+
+extern "C" int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F,
+                                        int32_t item_col, const void* E, int64_t features_M,
+                                        int32_t k, int32_t dtype, const float* w,
+                                        int32_t nlayers, const int32_t* layer_dims,
+                                        const void* const* Wt, const float* const* bias,
+                                        int32_t mlp_dtype, const float* Wp, float bp,
+                                        int32_t item_row_begin, int32_t item_count,
+                                        int32_t global_item_base, int32_t K, int64_t chunk_rows,
+                                        float* top_score, int32_t* top_idx, int32_t proj_mode,
+                                        void* workspace, size_t ws_bytes, void* stream) {
+  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
+  return dfm_catalog_run(qidx, B, F, item_col, E, features_M, k, dtype, w, nlayers, layer_dims,
+                         Wt, bias, mlp_dtype, Wp, bp, item_row_begin, item_count,
+                         global_item_base, K, chunk_rows, top_score, top_idx, workspace,
+                         ws_bytes, proj_mode, stream);
 }
 
 extern "C" int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,

@@ -225,8 +225,8 @@ PYBIND11_MODULE(_hhfm, m) {
   m.def("dfm_forward",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w,
            std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
-           int mlp_dtype, uptr Wp, float bp, uptr out, uptr ws, size_t ws_bytes,
-           uptr stream) {
+           int mlp_dtype, uptr Wp, float bp, uptr out, int proj_mode, uptr ws,
+           size_t ws_bytes, uptr stream) {
           if (Wt.size() != dims.size() || bias.size() != dims.size())
             throw py::value_error("dims, Wt and bias must have the same length");
           std::vector<const void*> W(Wt.size());
@@ -238,12 +238,13 @@ PYBIND11_MODULE(_hhfm, m) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_dfm_forward(P<const int32_t>(idx), B, F, P<const void>(E), M, k, dtype,
-                                  P<const float>(w), (int)dims.size(), dims.data(), W.data(),
-                                  b.data(), mlp_dtype, P<const float>(Wp), bp, P<float>(out),
-                                  P<void>(ws), ws_bytes, P<void>(stream));
+            rc = hhfm_dfm_forward_ex(P<const int32_t>(idx), B, F, P<const void>(E), M, k,
+                                     dtype, P<const float>(w), (int)dims.size(), dims.data(),
+                                     W.data(), b.data(), mlp_dtype, P<const float>(Wp), bp,
+                                     P<float>(out), proj_mode, P<void>(ws), ws_bytes,
+                                     P<void>(stream));
           }
-          check(rc, "hhfm_dfm_forward");
+          check(rc, "hhfm_dfm_forward_ex");
         });
 
   m.def("dfm_catalog_topk_workspace",
@@ -272,7 +273,7 @@ PYBIND11_MODULE(_hhfm, m) {
            uptr w, std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
            int mlp_dtype, uptr Wp, float bp, int item_row_begin, int item_count,
            int global_item_base, int K, int64_t chunk_rows, uptr top_score, uptr top_idx,
-           uptr ws, size_t ws_bytes, uptr stream) {
+           int proj_mode, uptr ws, size_t ws_bytes, uptr stream) {
           if (Wt.size() != dims.size() || bias.size() != dims.size())
             throw py::value_error("dims, Wt and bias must have the same length");
           std::vector<const void*> W(Wt.size());
@@ -284,15 +285,15 @@ PYBIND11_MODULE(_hhfm, m) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_dfm_catalog_topk(P<const int32_t>(qidx), B, F, item_col, P<const void>(E),
-                                       M, k, dtype, P<const float>(w), (int)dims.size(),
-                                       dims.data(), W.data(), b.data(), mlp_dtype,
-                                       P<const float>(Wp), bp, item_row_begin, item_count,
-                                       global_item_base, K, chunk_rows, P<float>(top_score),
-                                       P<int32_t>(top_idx), P<void>(ws), ws_bytes,
-                                       P<void>(stream));
+            rc = hhfm_dfm_catalog_topk_ex(P<const int32_t>(qidx), B, F, item_col,
+                                          P<const void>(E), M, k, dtype, P<const float>(w),
+                                          (int)dims.size(), dims.data(), W.data(), b.data(),
+                                          mlp_dtype, P<const float>(Wp), bp, item_row_begin,
+                                          item_count, global_item_base, K, chunk_rows,
+                                          P<float>(top_score), P<int32_t>(top_idx), proj_mode,
+                                          P<void>(ws), ws_bytes, P<void>(stream));
           }
-          check(rc, "hhfm_dfm_catalog_topk");
+          check(rc, "hhfm_dfm_catalog_topk_ex");
         });
 
   m.def("afm_forward_workspace", [](int64_t B, int F, int A) {

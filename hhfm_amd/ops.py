@@ -214,17 +214,19 @@ def dfm_prepare_weights(layers, biases, mlp_dtype: torch.dtype, F: int, k: int):
     return Wt, bs, dims
 
 
-DFM_PROJ = {False: 0, True: 1, None: 2}   # include/hhfm.h hhfm_dfm_proj: off / on / auto
+# include/hhfm.h hhfm_dfm_proj: off / on / auto / context fields only
+DFM_PROJ = {False: 0, True: 1, None: 2, "ctx": 3}
 
 
 def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                 mlp_dtype: torch.dtype, Wp: torch.Tensor, bp: float,
                 out: Optional[torch.Tensor] = None,
-                proj: Optional[bool] = None) -> torch.Tensor:
+                proj=None) -> torch.Tensor:
     """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B].
 
     ``proj``: projected layer 0 (include/hhfm.h, ABI v3) — None lets the
-    library decide (rows >= 2 x table rows), True / False force it on / off."""
+    library decide (rows >= 2 x table rows), True / False force it on / off,
+    "ctx" projects the context fields 2..F-1 only (bf16 MLP)."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, Wp, *Wt, *bias)
     B, F = idx.shape
@@ -237,19 +239,17 @@ def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, d
     nat = native()
     nbytes = nat.dfm_forward_workspace_ex(B, F, k, M, list(dims), md, DFM_PROJ[proj])
     ws = _workspace(dev, nbytes)
-    # the planned size, not the (cached, possibly larger) buffer's: the
-    # library picks the projected path from the size it is handed
     nat.dfm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
                     list(dims), [t.data_ptr() for t in Wt], [t.data_ptr() for t in bias], md,
-                    Wp.data_ptr(), float(bp), out.data_ptr(), ws.data_ptr(), nbytes,
-                    _stream(dev))
+                    Wp.data_ptr(), float(bp), out.data_ptr(), DFM_PROJ[proj], ws.data_ptr(),
+                    ws.numel(), _stream(dev))
     return out
 
 
 def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                      Wp: torch.Tensor, bp: float, item_col: int, item_row_begin: int,
                      item_count: int, K: int, global_item_base: int = 0,
-                     chunk_rows: int = 1 << 20, proj: Optional[bool] = None):
+                     chunk_rows: int = 1 << 20, proj=None):
     """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K]); ``proj`` as
     in :func:`dfm_forward` (rows = B x item_count)."""
     _idx(qidx, "qidx")
@@ -267,8 +267,8 @@ def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, b
                          w.data_ptr(), list(dims), [t.data_ptr() for t in Wt],
                          [t.data_ptr() for t in bias], md, Wp.data_ptr(), float(bp),
                          item_row_begin, item_count, global_item_base, K, chunk_rows,
-                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), nbytes,
-                         _stream(dev))
+                         top_s.data_ptr(), top_i.data_ptr(), DFM_PROJ[proj], ws.data_ptr(),
+                         ws.numel(), _stream(dev))
     return top_s, top_i
 
 

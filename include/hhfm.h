@@ -177,21 +177,27 @@ int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_
 
 /* Projected layer 0 (ABI v3).  Layer 0 is linear before its ReLU, so
  * h_0 = Σ_f P_f[x_f] with P_f[id] = W0[:, f·k:(f+1)·k] · E[id]: the forward
- * computes P for every table row and field once per call (F MFMA GEMMs, the
- * direct kernel's operand rounding, fp32 results) and the fused kernel
- * gathers it instead
- * of streaming layer 0's weights — a saving when rows >= 2·features_M
- * (DFM.py:125-128 computed by the same products, summed per field first).
- * hhfm_dfm_forward / hhfm_dfm_catalog_topk take that path when ws_bytes
- * covers the projected plan (the *_workspace_ex size with proj_mode != OFF)
- * and the shape is inside the fused envelope (k % 16 == 0, k <= 512, F <= 16,
- * <= 4 layers of <= 416 units); otherwise the direct kernels run.
- * P needs F·features_M·32·⌈max width/32⌉ floats (at most 1 GiB planned). */
+ * computes P for every table row of the projected fields once per call (MFMA
+ * GEMMs, the direct kernel's operand rounding, fp32 results) and the fused
+ * kernel gathers it instead of streaming those fields' layer-0 weights — a
+ * saving when rows >= 2·features_M (DFM.py:125-128 computed by the same
+ * products, summed per field first).
+ * The *_ex entry points take proj_mode explicitly; hhfm_dfm_forward /
+ * hhfm_dfm_catalog_topk project every field when ws_bytes covers that plan
+ * (the *_workspace_ex size with HHFM_DFM_PROJ_ON) and run direct otherwise.
+ * Projection needs the fused envelope (k % 16 == 0, k <= 512, F <= 16,
+ * <= 4 layers of <= 416 units); outside it every mode runs direct.
+ * P needs (F - first projected field)·features_M·32·⌈max width/32⌉ floats
+ * (at most 1 GiB planned). */
 enum hhfm_dfm_proj {
   HHFM_DFM_PROJ_OFF = 0,  /* plan the direct path only                       */
-  HHFM_DFM_PROJ_ON = 1,   /* plan P whenever the shape admits it             */
-  HHFM_DFM_PROJ_AUTO = 2  /* plan P for the fp32 MLP when rows (B, or
-                             B·item_count) >= 2·M; bf16 MLP stays direct     */
+  HHFM_DFM_PROJ_ON = 1,   /* project every field                             */
+  HHFM_DFM_PROJ_AUTO = 2, /* when rows (B, or B·item_count) >= 2·M: ON for
+                             the fp32 MLP, CTX for the bf16 MLP             */
+  HHFM_DFM_PROJ_CTX = 3   /* bf16 MLP, F >= 3: project the context fields
+                             2..F-1 (LoadData's layout: user, item,
+                             contexts), fields 0 and 1 stay on MFMA; other
+                             shapes run direct                               */
 };
 int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k, int64_t features_M,
                                   int32_t nlayers, const int32_t* layer_dims,
@@ -202,6 +208,14 @@ int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
                      const float* const* bias, int32_t mlp_dtype, const float* Wp,
                      float bp, float* out, void* workspace, size_t ws_bytes,
                      void* stream);
+/* Same, with the projection mode explicit; ws_bytes must cover
+ * hhfm_dfm_forward_workspace_ex(..., proj_mode). */
+int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                        int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                        int32_t nlayers, const int32_t* layer_dims, const void* const* Wt,
+                        const float* const* bias, int32_t mlp_dtype, const float* Wp,
+                        float bp, float* out, int32_t proj_mode, void* workspace,
+                        size_t ws_bytes, void* stream);
 
 /* D2 — DeepFM.topk (DFM.py:219-231): every query row is tiled over the
  * catalog with column item_col replaced by each item id, scored by D1 and
@@ -224,6 +238,16 @@ int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t ite
                           int32_t global_item_base, int32_t K, int64_t chunk_rows,
                           float* top_score, int32_t* top_idx, void* workspace,
                           size_t ws_bytes, void* stream);
+/* Same, with the projection mode explicit (see hhfm_dfm_forward_ex). */
+int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
+                             const void* E, int64_t features_M, int32_t k, int32_t dtype,
+                             const float* w, int32_t nlayers, const int32_t* layer_dims,
+                             const void* const* Wt, const float* const* bias,
+                             int32_t mlp_dtype, const float* Wp, float bp,
+                             int32_t item_row_begin, int32_t item_count,
+                             int32_t global_item_base, int32_t K, int64_t chunk_rows,
+                             float* top_score, int32_t* top_idx, int32_t proj_mode,
+                             void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * A1 — AFM per-row score (replaces `AFM.out`, AFM.py:103-142), attention on,

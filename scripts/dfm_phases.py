@@ -49,10 +49,10 @@ for mdt in (torch.bfloat16,):
             m.validate = False
             Wt, bs, dims, Wp, bp = m._prepared()
             out = torch.empty(B, device=dev)
-            for pj in (False, True):
+            for pj in (False, True, "ctx"):
                 fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1),  # noqa
                                              Wt, bs, dims, mdt, Wp, bp, out=out, proj=pj)
-                key = f"{'bf16' if mdt == torch.bfloat16 else 'f32'}mlp_{'tbf16' if tdt == torch.bfloat16 else 'tf32'}_L{len(layers)}_{'proj' if pj else 'direct'}"
+                key = f"{'bf16' if mdt == torch.bfloat16 else 'f32'}mlp_{'tbf16' if tdt == torch.bfloat16 else 'tf32'}_L{len(layers)}_{ {False: 'direct', True: 'proj', 'ctx': 'ctx'}[pj] }"
                 res[key] = round(timeit(fn), 4)
             del m
             torch.cuda.empty_cache()

@@ -161,9 +161,9 @@ def test_wide_ids_are_checked_before_narrowing():
 
 
 def test_dfm_projection_auto_plan():
-    """ABI v3 planning: AUTO plans P for the fp32 MLP exactly when rows >= 2 x
-    table rows (the projected workspace is what ON reports) and never for the
-    bf16 MLP; ON plans it for both."""
+    """ABI v3 planning: AUTO plans P exactly when rows >= 2 x table rows —
+    every field for the fp32 MLP (ON's workspace), the context fields for the
+    bf16 MLP (CTX's); ON plans every field for both."""
     from hhfm_amd._native import native
     nat = native()
     dims = [400, 400, 400]
@@ -172,10 +172,22 @@ def test_dfm_projection_auto_plan():
         on = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 1)
         assert on - off >= 5 * 5051 * 416 * 4   # fp32 P
         auto = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 2)
-        assert auto == (on if md == 0 else off)
+        ctx = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 3)
+        assert auto == (on if md == 0 else ctx) and (md == 0 or off < ctx < on)
         small = nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 2)
         assert small == nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 0)
         assert off == nat.dfm_forward_workspace(1 << 20, dims, md)
+    # CTX: P for fields 2..F-1 only, bf16 MLP only
+    off = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 0)
+    ctx = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 3)
+    on = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 1)
+    assert ctx - off >= 3 * 5051 * 416 * 4 and ctx < on
+    assert (nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 0, 3)
+            == nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 0, 0))
+    assert (nat.dfm_forward_workspace_ex(1 << 20, 2, 256, 5051, dims, 1, 3)
+            == nat.dfm_forward_workspace_ex(1 << 20, 2, 256, 5051, dims, 1, 0))
+    with pytest.raises(ValueError):
+        nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 4)
     # outside the fused envelope (k % 16 != 0) nothing is planned
     assert (nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 1)
             == nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 0))

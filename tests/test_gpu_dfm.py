@@ -107,7 +107,7 @@ def test_dfm_forward_shapes(mlp, k, layers):
         assert np.all(np.abs(got - ref) <= 5e-3 * mag)
 
 
-@pytest.mark.parametrize("proj", [False, True])
+@pytest.mark.parametrize("proj", [False, True, "ctx"])
 @pytest.mark.parametrize("mlp", ["f32", "bf16"])
 def test_dfm_catalog_topk_chunked(mlp, proj):
     """Query chunking (chunk_rows < B*N) gives the same top-K as one pass
@@ -198,12 +198,14 @@ def test_dfm_fused_envelope(F, k, layers, tdt, B, mlp):
     (3, 48, [64, 96, 33, 20], "f32", 1000),     # 4 layers, odd widths
     (11, 32, [128, 416], "bf16", 1),            # widest envelope, one row
 ])
-@pytest.mark.parametrize("mlp", ["bf16", "f32"])
-def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp):
+@pytest.mark.parametrize("mlp,proj", [("bf16", True), ("f32", True), ("bf16", "ctx")])
+def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
     """Projected layer 0 (h_0 = Σ_f P_f[x_f], dfm_fused.hip PROJ kernels),
-    forced on, against the same oracles and tolerances as the direct kernels,
-    and against the direct kernel itself (bf16: summation order only, so the
-    two differ by at most a bf16 flip of a hidden unit)."""
+    forced on for every field (True) or for the context fields 2..F-1 with
+    fields 0, 1 on MFMA ("ctx", bf16 MLP), against the same oracles and
+    tolerances as the direct kernels, and against the direct kernel itself
+    (bf16: summation order only, so the two differ by at most a bf16 flip of
+    a hidden unit)."""
     from hhfm_amd import ops
     rng = np.random.default_rng(F * 7919 + k)
     M = 997
@@ -222,7 +224,7 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp):
     Wt, bs, dims, Wpd, bpd = m._prepared()
     xd = torch.from_numpy(X).cuda()
     wb = m.weights["feature_bias"].reshape(-1)
-    got = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, mdt, Wpd, bpd, proj=True).cpu().numpy()
+    got = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, mdt, Wpd, bpd, proj=proj).cpu().numpy()
     direct = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, mdt, Wpd, bpd,
                              proj=False).cpu().numpy()
     mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
