@@ -56,6 +56,7 @@ constexpr int kFusedMaxLayers = 4;
 constexpr int kFusedMaxF = 16;
 constexpr int kFusedMaxK = 512;
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
+constexpr int kLdsBytes = 160 * 1024;   // gfx950 LDS per workgroup
 
 struct FusedDfmArgs {
   const int32_t* idx;
@@ -128,6 +129,11 @@ __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, 
   }
 }
 
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
 template <bool TBF, int TM, bool PROJ>
 __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   constexpr int NR = TM * 32;                // weight rows per chunk
@@ -136,7 +142,15 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   constexpr int kW = 2 * CU * 16;
   constexpr int kIds = kW, kBl = kIds + kFusedRows * kFusedMaxF * 4;
   constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
-  constexpr int kSmem = kWp + (kFusedMaxF + kFusedMaxK) * 4;
+  constexpr int kPlo = kWp + (kFusedMaxF + kFusedMaxK) * 4;   // PROJ: per-field id span
+  // PROJ: the rest of the LDS stages P rows of projected fields whose ids in
+  // this block span few table rows (row stride NR + 4 floats: rows of distinct
+  // ids start 4 banks apart)
+  constexpr int kPst = kPlo + 4 * kFusedMaxF * 4;
+  constexpr int kPsLd = NR + 4;
+  constexpr int kPsFloats = PROJ ? (kLdsBytes - kPst) / 4 : 0;
+  constexpr int kSmem = kPst + kPsFloats * 4;
+  static_assert(kSmem <= kLdsBytes, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[kSmem];
   uint4* wbuf0 = reinterpret_cast<uint4*>(smem);   // [2][NR rows][8 slots]
   int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
@@ -163,6 +177,11 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
   // Wp: [0, F) the Σw weights, [kFusedMaxF, +k) the FM columns (16-B aligned)
   for (int x = tid; x < F + k; x += 256) wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x];
+  int* plo = reinterpret_cast<int*>(smem + kPlo);   // [0,16) lo, [16,32) hi, [32,48) LDS base
+  if (PROJ && tid < kFusedMaxF) {
+    plo[tid] = 0x7fffffff;
+    plo[kFusedMaxF + tid] = -1;
+  }
   // layer-0 K order is c-major: step S covers field S%F, columns 16(S/F)..+15.
   // Padding steps (S >= nS) multiply zero weights and skip the FM part.
 
@@ -218,288 +237,368 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     }
   };
 
-  f32x16 acc[TM];
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int x = 0; x < 16; ++x) acc[t][x] = 0.f;
-  float fs[8], fq[8];
-  float y2 = 0.f;
-
   __syncthreads();   // ids, step tables visible
 
-  // Per K-chunk g (buffer g&1): DMA chunk g+1 into the other buffer (read in
-  // chunk g-1, released by its barrier), load the next embedding chunk into
-  // the other register set, run chunk g's MFMAs, then vmcnt(0) + barrier
-  // (__syncthreads) publishes chunk g+1.
-
-  // One 64-deep chunk from LDS buffer b: the TM weight fragments of step
-  // j+1 are read right behind step j's MFMAs (software pipelined; one wave
-  // per SIMD has no other wave to hide LDS latency), bop(j) supplies the B
-  // operand of step j and side(j) runs beside it.
-  auto run_chunk = [&](int b, auto&& bop, auto&& side) {
-    bf16x8 fa[TM];
-#pragma unroll
-    for (int t = 0; t < TM; ++t) fa[t] = wfrag(b, t, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bf16x8 bb = bop(j);
-#pragma unroll
-      for (int t = 0; t < TM; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t], bb, acc[t], 0, 0, 0);
-        if (j < 3) fa[t] = wfrag(b, t, j + 1);
-        __builtin_amdgcn_sched_barrier(0);   // keep the read right behind its MFMA
-      }
-      side(j);
-    }
-  };
-
+  // Projected fields whose ids in this block span few table rows (Frappe's
+  // context fields: 7, 2, 3 rows) are staged in LDS, P rows and table rows:
+  // the block's id span per field by LDS atomics over its 128 rows (tail rows
+  // hold id 0); the body is instantiated twice (staged / HBM) and the block
+  // picks one — a runtime select between LDS and HBM addresses would compile
+  // to flat loads inside the MFMA loop.
+  const int ek = TBF ? k / 2 : k;   // table row in floats
+  bool allfit = false;
   if constexpr (PROJ) {
-    // ----- projected layer 0: acc = Σ_{f >= Fd} P_f[x_f]; with Fd == 0 also
-    // the FM part from the table (otherwise the direct loop below adds the
-    // MFMA part of fields < Fd and the FM part) -----
-    if (Fd == 0 && nchunks > 0) dma(0, 0);   // hidden chunk 0 streams behind the gathers
-    // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
-    // one float4 of P per (field, tile, g); all 4·TM of a field in flight.
-    // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
-    // HHFM_KO_PROJFM skip the P / FM loads — scripts/build_variants.sh.)
-#ifndef HHFM_KO_PROJP
-    for (int f = Fd; f < F; ++f) {
-      // P in accumulator order: positions 32t + 16h .. +15 are this lane's
-      // units of tile t (64 contiguous bytes)
-      const float4* pp = reinterpret_cast<const float4*>(
-                             reinterpret_cast<const float*>(a.proj) + (f - Fd) * a.proj_fstride +
-                             (int64_t)ids[myrow * F + f] * a.proj_ld) + 4 * h;
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const float4 x = pp[8 * t + g4];
-          acc[t][4 * g4 + 0] += x.x;
-          acc[t][4 * g4 + 1] += x.y;
-          acc[t][4 * g4 + 2] += x.z;
-          acc[t][4 * g4 + 3] += x.w;
-        }
+    for (int x = tid; x < kFusedRows * (F - Fd); x += 256) {
+      const int row = x / (F - Fd), f = Fd + x % (F - Fd);
+      atomicMin(&plo[f], ids[row * F + f]);
+      atomicMax(&plo[kFusedMaxF + f], ids[row * F + f]);
     }
-#endif
-    // FM second-order part (DFM.py:114-122): the lane half h takes columns
-    // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
-    for (int j = 0; j < (Fd == 0 ? k / 16 : 0); ++j) {
-#ifndef HHFM_KO_PROJFM
-      float s8[8], q8[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) { s8[q] = 0.f; q8[q] = 0.f; }
-      for (int f = 0; f < F; ++f) {
-        const int64_t id = ids[myrow * F + f];
-        float v[8];
-        if constexpr (TBF) {
-          const uint4 x = *reinterpret_cast<const uint4*>(
-              reinterpret_cast<const uint16_t*>(a.E) + id * k + 16 * j + 8 * h);
-          const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[2 * q] = __uint_as_float(x4[q] << 16);
-            v[2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
-          }
-        } else {
-          const float4* p = reinterpret_cast<const float4*>(
-              reinterpret_cast<const float*>(a.E) + id * k + 16 * j + 8 * h);
-          const float4 p0 = p[0], p1 = p[1];
-          v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
-          v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          s8[q] += v[q];
-          q8[q] += v[q] * v[q];
-        }
-      }
-      const float4* wc = reinterpret_cast<const float4*>(wpl + kFusedMaxF + 16 * j + 8 * h);
-      const float4 w0 = wc[0], w1 = wc[1];
-      const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      float d = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) d += 0.5f * (s8[q] * s8[q] - q8[q]) * wq[q];
-      y2 += d;
-#endif
-    }
-    if (Fd == 0) __syncthreads();   // vmcnt(0): hidden chunk 0 landed
+    __syncthreads();
+    int64_t need = 0;
+    for (int f = Fd; f < F; ++f)
+      need += (int64_t)(plo[kFusedMaxF + f] - plo[f] + 1) * (kPsLd + ek);
+    allfit = need <= kPsFloats;
   }
-  if (!PROJ || Fd > 0) {
-  EChunk e0, e1;
-  Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
-  eload(e0, cg);
-  dma(0, 0);
-  __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
-  // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
-  // Chunk c first turns the embeddings gathered during chunk c-1 into its 4
-  // B operands (and the fp32 values of the FM part), THEN issues chunk c+1's
-  // weight DMA and gathers into the freed registers: the compiler's wait on
-  // the gathered registers (it cannot count loads across the loop's back
-  // edge, so it is a vmcnt(0)) then lands before the new loads, not after.
-  auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
-    const int b = c & 1;
-    float v[4][8];
-    uint4 bxs[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (TBF) {
-        bxs[j] = e.v[j];   // already the B operand; fp32 values made per step
-      } else {
-        const uint4 p = e.v[2 * j], q = e.v[2 * j + 1];
-        v[j][0] = __uint_as_float(p.x); v[j][1] = __uint_as_float(p.y);
-        v[j][2] = __uint_as_float(p.z); v[j][3] = __uint_as_float(p.w);
-        v[j][4] = __uint_as_float(q.x); v[j][5] = __uint_as_float(q.y);
-        v[j][6] = __uint_as_float(q.z); v[j][7] = __uint_as_float(q.w);
-        bxs[j] = make_uint4(pack_bf16x2(v[j][0], v[j][1]), pack_bf16x2(v[j][2], v[j][3]),
-                            pack_bf16x2(v[j][4], v[j][5]), pack_bf16x2(v[j][6], v[j][7]));
-      }
-    }
-    // then the next chunk's weight DMA and gathers, in one burst
-    // (measured: placing them one per MFMA gap instead ran 6-7 % slower)
-    if (c + 1 < nchunks) dma(c + 1, b ^ 1);
-    if (c + 1 < nc0) eload(en, cg);
-    auto bop = [&](int j) {
-      if constexpr (TBF) {
-        const uint32_t x4[4] = {bxs[j].x, bxs[j].y, bxs[j].z, bxs[j].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[j][2 * q] = __uint_as_float(x4[q] << 16);
-          v[j][2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
+  auto body = [&](auto stc) {
+    constexpr bool ST = decltype(stc)::value;
+    f32x16 acc[TM];
+  #pragma unroll
+    for (int t = 0; t < TM; ++t)
+  #pragma unroll
+      for (int x = 0; x < 16; ++x) acc[t][x] = 0.f;
+    float fs[8], fq[8];
+    float y2 = 0.f;
+
+    // Per K-chunk g (buffer g&1): DMA chunk g+1 into the other buffer (read in
+    // chunk g-1, released by its barrier), load the next embedding chunk into
+    // the other register set, run chunk g's MFMAs, then vmcnt(0) + barrier
+    // (__syncthreads) publishes chunk g+1.
+
+    // One 64-deep chunk from LDS buffer b: the TM weight fragments of step
+    // j+1 are read right behind step j's MFMAs (software pipelined; one wave
+    // per SIMD has no other wave to hide LDS latency), bop(j) supplies the B
+    // operand of step j and side(j) runs beside it.
+    auto run_chunk = [&](int b, auto&& bop, auto&& side) {
+      bf16x8 fa[TM];
+  #pragma unroll
+      for (int t = 0; t < TM; ++t) fa[t] = wfrag(b, t, 0);
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 bb = bop(j);
+  #pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t], bb, acc[t], 0, 0, 0);
+          if (j < 3) fa[t] = wfrag(b, t, j + 1);
+          __builtin_amdgcn_sched_barrier(0);   // keep the read right behind its MFMA
         }
+        side(j);
       }
-      return __builtin_bit_cast(bf16x8, bxs[j]);
     };
-    // FM second-order part over the same values (DFM.py:114-122)
-    auto side = [&](int j) {
-      const int f = cs.S < nS ? cs.f : -1;
-      if (f == 0) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) { fs[q] = 0.f; fq[q] = 0.f; }
+
+    if constexpr (PROJ) {
+      // ----- ST: the block's projected fields' P rows and table rows, rows
+      // lo..hi of each, staged in LDS (read below instead of HBM) -----
+      float* pst = reinterpret_cast<float*>(smem + kPst);
+      const float* P = reinterpret_cast<const float*>(a.proj);
+      if constexpr (ST) {
+        int used = 0;
+        for (int f = Fd; f < F; ++f) {
+          const int lo = plo[f], span = plo[kFusedMaxF + f] - lo + 1;
+          for (int x = tid; x < span * (NR / 4); x += 256) {
+            const int row = x / (NR / 4), c4 = x % (NR / 4);
+            *reinterpret_cast<float4*>(pst + used + row * kPsLd + 4 * c4) =
+                *reinterpret_cast<const float4*>(P + (f - Fd) * a.proj_fstride +
+                                                 (int64_t)(lo + row) * a.proj_ld + 4 * c4);
+          }
+          const float4* Ef = reinterpret_cast<const float4*>(
+              reinterpret_cast<const float*>(a.E) + (int64_t)lo * ek);
+          float4* dst = reinterpret_cast<float4*>(pst + used + span * kPsLd);
+          for (int x = tid; x < span * ek / 4; x += 256) dst[x] = Ef[x];
+          if (tid == 0) {
+            plo[2 * kFusedMaxF + f] = used;                  // P rows
+            plo[3 * kFusedMaxF + f] = used + span * kPsLd;   // table rows
+          }
+          used += span * (kPsLd + ek);
+        }
+        __syncthreads();
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        fs[q] += v[j][q];
-        fq[q] += v[j][q] * v[j][q];
+      // ----- projected layer 0: acc = Σ_{f >= Fd} P_f[x_f]; with Fd == 0 also
+      // the FM part from the table (otherwise the direct loop below adds the
+      // MFMA part of fields < Fd and the FM part) -----
+      if (Fd == 0 && nchunks > 0) dma(0, 0);   // hidden chunk 0 streams behind the gathers
+      // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
+      // one float4 of P per (field, tile, g); all 4·TM of a field in flight.
+      // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
+      // HHFM_KO_PROJFM skip the P / FM loads — scripts/build_variants.sh.)
+  #ifndef HHFM_KO_PROJP
+      for (int f = Fd; f < F; ++f) {
+        // P in accumulator order: positions 32t + 16h .. +15 are this lane's
+        // units of tile t (64 contiguous bytes), from LDS when staged
+        auto addp = [&](const float4* pp) {
+  #pragma unroll
+          for (int t = 0; t < TM; ++t)
+  #pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const float4 x = pp[8 * t + g4];
+              acc[t][4 * g4 + 0] += x.x;
+              acc[t][4 * g4 + 1] += x.y;
+              acc[t][4 * g4 + 2] += x.z;
+              acc[t][4 * g4 + 3] += x.w;
+            }
+        };
+        if constexpr (ST)
+          addp(reinterpret_cast<const float4*>(pst + plo[2 * kFusedMaxF + f] +
+                                               (ids[myrow * F + f] - plo[f]) * kPsLd) +
+               4 * h);
+        else
+          addp(reinterpret_cast<const float4*>(P + (f - Fd) * a.proj_fstride +
+                                               (int64_t)ids[myrow * F + f] * a.proj_ld) +
+               4 * h);
       }
-      if (f == Fd - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
-        if constexpr (PROJ) {
-          // the projected fields' values of these 8 columns (their rows are
-          // few and cache-resident: Frappe's contexts)
-          for (int f2 = Fd; f2 < F; ++f2) {
-            const int64_t id2 = ids[myrow * F + f2];
-            float u8[8];
-            if constexpr (TBF) {
-              const uint4 x = *reinterpret_cast<const uint4*>(
-                  reinterpret_cast<const uint16_t*>(a.E) + id2 * k + cs.col + 8 * h);
-              const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-              for (int qq = 0; qq < 4; ++qq) {
-                u8[2 * qq] = __uint_as_float(x4[qq] << 16);
-                u8[2 * qq + 1] = __uint_as_float(x4[qq] & 0xffff0000u);
-              }
-            } else {
-              const float4* p2 = reinterpret_cast<const float4*>(
-                  reinterpret_cast<const float*>(a.E) + id2 * k + cs.col + 8 * h);
-              const float4 p0 = p2[0], p1 = p2[1];
-              u8[0] = p0.x; u8[1] = p0.y; u8[2] = p0.z; u8[3] = p0.w;
-              u8[4] = p1.x; u8[5] = p1.y; u8[6] = p1.z; u8[7] = p1.w;
+  #endif
+      // FM second-order part (DFM.py:114-122): the lane half h takes columns
+      // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
+      for (int j = 0; j < (Fd == 0 ? k / 16 : 0); ++j) {
+  #ifndef HHFM_KO_PROJFM
+        float s8[8], q8[8];
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) { s8[q] = 0.f; q8[q] = 0.f; }
+        for (int f = 0; f < F; ++f) {
+          const int64_t id = ids[myrow * F + f];
+          float v[8];
+          if constexpr (TBF) {
+            const uint4 x = *reinterpret_cast<const uint4*>(
+                reinterpret_cast<const uint16_t*>(a.E) + id * k + 16 * j + 8 * h);
+            const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
+  #pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[2 * q] = __uint_as_float(x4[q] << 16);
+              v[2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
             }
-#pragma unroll
-            for (int qq = 0; qq < 8; ++qq) {
-              fs[qq] += u8[qq];
-              fq[qq] += u8[qq] * u8[qq];
-            }
+          } else {
+            const float4* p = reinterpret_cast<const float4*>(
+                reinterpret_cast<const float*>(a.E) + id * k + 16 * j + 8 * h);
+            const float4 p0 = p[0], p1 = p[1];
+            v[0] = p0.x; v[1] = p0.y; v[2] = p0.z; v[3] = p0.w;
+            v[4] = p1.x; v[5] = p1.y; v[6] = p1.z; v[7] = p1.w;
+          }
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            s8[q] += v[q];
+            q8[q] += v[q] * v[q];
           }
         }
-        const float4* wc =
-            reinterpret_cast<const float4*>(wpl + kFusedMaxF + cs.col + 8 * h);
+        const float4* wc = reinterpret_cast<const float4*>(wpl + kFusedMaxF + 16 * j + 8 * h);
         const float4 w0 = wc[0], w1 = wc[1];
         const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
         float d = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) d += 0.5f * (fs[q] * fs[q] - fq[q]) * wq[q];
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) d += 0.5f * (s8[q] * s8[q] - q8[q]) * wq[q];
         y2 += d;
+  #endif
       }
-      adv(cs);
-    };
-    run_chunk(b, bop, side);
-    __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
-  };
-  // (two register sets alternate, so no copy of the gathered chunk is needed
-  // on the loop's back edge)
-  for (int c = 0; c < nc0; c += 2) {
-    chunk0(c, e0, e1);
-    if (c + 1 < nc0) chunk0(c + 1, e1, e0);
-  }
-  }   // direct layer 0
+      if (Fd == 0) __syncthreads();   // vmcnt(0): hidden chunk 0 landed
+    }
+    if (!PROJ || Fd > 0) {
+    EChunk e0, e1;
+    Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
+    eload(e0, cg);
+    dma(0, 0);
+    __syncthreads();   // vmcnt(0): chunk 0 in LDS
 
-  // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
-  uint32_t X[TM][8];
-  int g = nc0;
-  for (int i = 1; i < L; ++i) {
-    // epilogue of layer i-1: bias + ReLU (DFM.py:127-128, every layer), bf16,
-    // then into B-operand order (k = 8*half + j) with one swap per pair
-    const float* bli = blv + (i - 1) * NR;
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      float v[16];
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const float4 bq = *reinterpret_cast<const float4*>(bli + 32 * t + 8 * g4 + 4 * h);
-        const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[4 * g4 + e] = fmaxf(acc[t][4 * g4 + e] + bv[e], 0.f);
-          acc[t][4 * g4 + e] = 0.f;
+    // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
+    // Chunk c first turns the embeddings gathered during chunk c-1 into its 4
+    // B operands (and the fp32 values of the FM part), THEN issues chunk c+1's
+    // weight DMA and gathers into the freed registers: the compiler's wait on
+    // the gathered registers (it cannot count loads across the loop's back
+    // edge, so it is a vmcnt(0)) then lands before the new loads, not after.
+    auto chunk0 = [&](int c, EChunk& e, EChunk& en) {
+      const int b = c & 1;
+      float v[4][8];
+      uint4 bxs[4];
+  #pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (TBF) {
+          bxs[j] = e.v[j];   // already the B operand; fp32 values made per step
+        } else {
+          const uint4 p = e.v[2 * j], q = e.v[2 * j + 1];
+          v[j][0] = __uint_as_float(p.x); v[j][1] = __uint_as_float(p.y);
+          v[j][2] = __uint_as_float(p.z); v[j][3] = __uint_as_float(p.w);
+          v[j][4] = __uint_as_float(q.x); v[j][5] = __uint_as_float(q.y);
+          v[j][6] = __uint_as_float(q.z); v[j][7] = __uint_as_float(q.w);
+          bxs[j] = make_uint4(pack_bf16x2(v[j][0], v[j][1]), pack_bf16x2(v[j][2], v[j][3]),
+                              pack_bf16x2(v[j][4], v[j][5]), pack_bf16x2(v[j][6], v[j][7]));
         }
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) X[t][q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
-      swap_halves(X[t][0], X[t][2]);
-      swap_halves(X[t][1], X[t][3]);
-      swap_halves(X[t][4], X[t][6]);
-      swap_halves(X[t][5], X[t][7]);
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c, ++g) {
-      const int b = g & 1;
-      if (g + 1 < nchunks) dma(g + 1, b ^ 1);
-      auto bop = [&](int j) {   // step j = input tile 2c + j/2, k16 half j%2
-        const int tin = 2 * c + (j >> 1), s2 = 4 * (j & 1);
-        const uint4 bx = tin < TM ? make_uint4(X[tin][s2], X[tin][s2 + 1], X[tin][s2 + 2],
-                                               X[tin][s2 + 3])
-                                  : make_uint4(0, 0, 0, 0);
-        return __builtin_bit_cast(bf16x8, bx);
+      // then the next chunk's weight DMA and gathers, in one burst
+      // (measured: placing them one per MFMA gap instead ran 6-7 % slower)
+      if (c + 1 < nchunks) dma(c + 1, b ^ 1);
+      if (c + 1 < nc0) eload(en, cg);
+      auto bop = [&](int j) {
+        if constexpr (TBF) {
+          const uint32_t x4[4] = {bxs[j].x, bxs[j].y, bxs[j].z, bxs[j].w};
+  #pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[j][2 * q] = __uint_as_float(x4[q] << 16);
+            v[j][2 * q + 1] = __uint_as_float(x4[q] & 0xffff0000u);
+          }
+        }
+        return __builtin_bit_cast(bf16x8, bxs[j]);
       };
-      run_chunk(b, bop, [](int) {});
-      __syncthreads();
+      // FM second-order part over the same values (DFM.py:114-122)
+      auto side = [&](int j) {
+        const int f = cs.S < nS ? cs.f : -1;
+        if (f == 0) {
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) { fs[q] = 0.f; fq[q] = 0.f; }
+        }
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          fs[q] += v[j][q];
+          fq[q] += v[j][q] * v[j][q];
+        }
+        if (f == Fd - 1) {   // (a branch-free form, evaluated every step, ran 11 % slower)
+          if constexpr (PROJ) {
+            // the projected fields' values of these 8 columns (their rows are
+            // few and cache-resident: Frappe's contexts)
+            for (int f2 = Fd; f2 < F; ++f2) {
+              const int64_t id2 = ids[myrow * F + f2];
+              const int eb = plo[3 * kFusedMaxF + f2];   // ST: staged, no HBM round trip
+              float u8[8];
+              if constexpr (TBF) {
+                uint4 x;
+                if constexpr (ST)
+                  x = *reinterpret_cast<const uint4*>(
+                      reinterpret_cast<const uint16_t*>(smem + kPst + 4 * eb) +
+                      (id2 - plo[f2]) * k + cs.col + 8 * h);
+                else
+                  x = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(a.E) +
+                                                      id2 * k + cs.col + 8 * h);
+                const uint32_t x4[4] = {x.x, x.y, x.z, x.w};
+  #pragma unroll
+                for (int qq = 0; qq < 4; ++qq) {
+                  u8[2 * qq] = __uint_as_float(x4[qq] << 16);
+                  u8[2 * qq + 1] = __uint_as_float(x4[qq] & 0xffff0000u);
+                }
+              } else {
+                float4 p0, p1;
+                if constexpr (ST) {
+                  const float4* p2 = reinterpret_cast<const float4*>(
+                      reinterpret_cast<const float*>(smem + kPst + 4 * eb) + (id2 - plo[f2]) * k +
+                      cs.col + 8 * h);
+                  p0 = p2[0];
+                  p1 = p2[1];
+                } else {
+                  const float4* p2 = reinterpret_cast<const float4*>(
+                      reinterpret_cast<const float*>(a.E) + id2 * k + cs.col + 8 * h);
+                  p0 = p2[0];
+                  p1 = p2[1];
+                }
+                u8[0] = p0.x; u8[1] = p0.y; u8[2] = p0.z; u8[3] = p0.w;
+                u8[4] = p1.x; u8[5] = p1.y; u8[6] = p1.z; u8[7] = p1.w;
+              }
+  #pragma unroll
+              for (int qq = 0; qq < 8; ++qq) {
+                fs[qq] += u8[qq];
+                fq[qq] += u8[qq] * u8[qq];
+              }
+            }
+          }
+          const float4* wc =
+              reinterpret_cast<const float4*>(wpl + kFusedMaxF + cs.col + 8 * h);
+          const float4 w0 = wc[0], w1 = wc[1];
+          const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+          float d = 0.f;
+  #pragma unroll
+          for (int q = 0; q < 8; ++q) d += 0.5f * (fs[q] * fs[q] - fq[q]) * wq[q];
+          y2 += d;
+        }
+        adv(cs);
+      };
+      run_chunk(b, bop, side);
+      __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
+    };
+    // (two register sets alternate, so no copy of the gathered chunk is needed
+    // on the loop's back edge)
+    for (int c = 0; c < nc0; c += 2) {
+      chunk0(c, e0, e1);
+      if (c + 1 < nc0) chunk0(c + 1, e1, e0);
     }
-  }
+    }   // direct layer 0
 
-  // ---- last layer: relu(acc + b) · Wp_deep, FM part, bias terms ----
-  const float* blL = blv + (L - 1) * NR;
-  float part = 0.f;
-#pragma unroll
-  for (int t = 0; t < TM; ++t)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int n = 32 * t + 8 * g4 + 4 * h;
-      const float4 bq = *reinterpret_cast<const float4*>(blL + n);
-      const float4 vq = *reinterpret_cast<const float4*>(vl + n);
-      part += fmaxf(acc[t][4 * g4 + 0] + bq.x, 0.f) * vq.x;
-      part += fmaxf(acc[t][4 * g4 + 1] + bq.y, 0.f) * vq.y;
-      part += fmaxf(acc[t][4 * g4 + 2] + bq.z, 0.f) * vq.z;
-      part += fmaxf(acc[t][4 * g4 + 3] + bq.w, 0.f) * vq.w;
+    // ----- layers 1..L-1: B operand = the previous layer's output, in registers -----
+    uint32_t X[TM][8];
+    int g = nc0;
+    for (int i = 1; i < L; ++i) {
+      // epilogue of layer i-1: bias + ReLU (DFM.py:127-128, every layer), bf16,
+      // then into B-operand order (k = 8*half + j) with one swap per pair
+      const float* bli = blv + (i - 1) * NR;
+  #pragma unroll
+      for (int t = 0; t < TM; ++t) {
+        float v[16];
+  #pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 bq = *reinterpret_cast<const float4*>(bli + 32 * t + 8 * g4 + 4 * h);
+          const float bv[4] = {bq.x, bq.y, bq.z, bq.w};
+  #pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[4 * g4 + e] = fmaxf(acc[t][4 * g4 + e] + bv[e], 0.f);
+            acc[t][4 * g4 + e] = 0.f;
+          }
+        }
+  #pragma unroll
+        for (int q = 0; q < 8; ++q) X[t][q] = pack_bf16x2(v[2 * q], v[2 * q + 1]);
+        swap_halves(X[t][0], X[t][2]);
+        swap_halves(X[t][1], X[t][3]);
+        swap_halves(X[t][4], X[t][6]);
+        swap_halves(X[t][5], X[t][7]);
+      }
+  #pragma unroll
+      for (int c = 0; c < NC; ++c, ++g) {
+        const int b = g & 1;
+        if (g + 1 < nchunks) dma(g + 1, b ^ 1);
+        auto bop = [&](int j) {   // step j = input tile 2c + j/2, k16 half j%2
+          const int tin = 2 * c + (j >> 1), s2 = 4 * (j & 1);
+          const uint4 bx = tin < TM ? make_uint4(X[tin][s2], X[tin][s2 + 1], X[tin][s2 + 2],
+                                                 X[tin][s2 + 3])
+                                    : make_uint4(0, 0, 0, 0);
+          return __builtin_bit_cast(bf16x8, bx);
+        };
+        run_chunk(b, bop, [](int) {});
+        __syncthreads();
+      }
     }
-  part += __shfl_xor(part, 32, kWave);
-  y2 += __shfl_xor(y2, 32, kWave);
-  const int64_t m = m0 + myrow;
-  if (h == 0 && m < a.B) {
-    float y1 = 0.f;
-    for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
-    a.out[m] = ((y1 + y2) + a.bp) + part;
+
+    // ---- last layer: relu(acc + b) · Wp_deep, FM part, bias terms ----
+    const float* blL = blv + (L - 1) * NR;
+    float part = 0.f;
+  #pragma unroll
+    for (int t = 0; t < TM; ++t)
+  #pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int n = 32 * t + 8 * g4 + 4 * h;
+        const float4 bq = *reinterpret_cast<const float4*>(blL + n);
+        const float4 vq = *reinterpret_cast<const float4*>(vl + n);
+        part += fmaxf(acc[t][4 * g4 + 0] + bq.x, 0.f) * vq.x;
+        part += fmaxf(acc[t][4 * g4 + 1] + bq.y, 0.f) * vq.y;
+        part += fmaxf(acc[t][4 * g4 + 2] + bq.z, 0.f) * vq.z;
+        part += fmaxf(acc[t][4 * g4 + 3] + bq.w, 0.f) * vq.w;
+      }
+    part += __shfl_xor(part, 32, kWave);
+    y2 += __shfl_xor(y2, 32, kWave);
+    const int64_t m = m0 + myrow;
+    if (h == 0 && m < a.B) {
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
+      a.out[m] = ((y1 + y2) + a.bp) + part;
+    }
+  };
+  if constexpr (PROJ) {
+    if (allfit) body(BoolC<true>{});
+    else body(BoolC<false>{});
+  } else {
+    body(BoolC<false>{});
   }
 }
 

@@ -154,6 +154,7 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   int from = -1;
   if (mode == HHFM_DFM_PROJ_ON) from = 0;
   if (mode == HHFM_DFM_PROJ_CTX && mlp_dtype == HHFM_BF16 && F >= 3) from = 2;
+  if (from == 2 && getenv("HHFM_EXP_FROM")) from = atoi(getenv("HHFM_EXP_FROM"));  // EXPERIMENT
   if (from >= 0 && M > 0 && dfm_proj_eligible(F, k, nlayers, dims)) {
     const size_t pb = dfm_proj_bytes(F, from, M, nlayers, dims);
     if (pb <= kProjMaxBytes) {

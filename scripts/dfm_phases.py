@@ -42,8 +42,8 @@ for c in (7, 2, 3):
 X = torch.stack(cols, 1).to(torch.int32).contiguous()
 res = {}
 for mdt in (torch.bfloat16,):
-    for tdt in (torch.float32, torch.bfloat16):
-        for layers in ([400], [400, 400], [400, 400, 400]):
+    for tdt in [torch.float32, torch.bfloat16][int(os.environ.get("PH_T0", 0)):]:
+        for layers in [[400], [400, 400], [400, 400, 400]][int(os.environ.get("PH_L0", 0)):]:
             m = DeepFM(nu, ni, M, 5, 256, layers, None, 0.01, 0, 0.0, device=dev,
                        mlp_dtype=mdt, table_dtype=tdt)
             m.validate = False

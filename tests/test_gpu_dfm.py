@@ -213,6 +213,12 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
     mdt = torch.bfloat16 if mlp == "bf16" else torch.float32
     m = _model((100, 200, M, F, k, layers), mlp_dtype=mdt, table_dtype=tdtype)
     X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    if proj == "ctx" and F >= 5:
+        # narrow context fields; field 4 narrow in the first half of the rows
+        # only: those blocks run LDS-staged (PJ = 2), the rest from HBM
+        X[:, 2] = 900 + X[:, 2] % 7
+        X[:, 3] = 950 + X[:, 3] % 2
+        X[:B // 2, 4] = 980 + X[:B // 2, 4] % 3
     W = m.get_weights()
     L = len(layers)
     Ls = [W[f"layer_{i}"] for i in range(L)]
