@@ -44,6 +44,8 @@
 // straight into the accumulator layout and runs the hidden layers as before.
 //
 // out[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c]) + bp) + Σ_n relu(h_L)·Wp[F+k+n]
+#include <hipcub/hipcub.hpp>
+
 #include "gemm_mfma.h"
 
 
@@ -57,6 +59,7 @@ constexpr int kFusedMaxF = 16;
 constexpr int kFusedMaxK = 512;
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
 constexpr int kLdsBytes = 160 * 1024;   // gfx950 LDS per workgroup
+constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
 
 struct FusedDfmArgs {
   const int32_t* idx;
@@ -82,6 +85,12 @@ struct FusedDfmArgs {
   int proj_ld;           // 32·TM
   int Fd;                // fields [0, Fd) run layer 0 on MFMA, [Fd, F) come from P
                          // (Fd = F: no projection; 0: all fields projected)
+  // bf16 kernel: internal field j is the caller's field (perm >> 4j) & 15
+  // (direct fields first), and block row m is the caller's row order[m]
+  // (rows grouped so that a projected field's ids stage in LDS); order may be
+  // null.  The fp32 kernel takes the identity.
+  uint64_t perm;
+  const int32_t* order;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -117,7 +126,7 @@ __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, 
       i = 0;
       const int S = 4 * g + (u >> 1);
       ok = S < nS;
-      kk = (S % Fd) * a.k + 16 * (S / Fd) + 8 * (u & 1);
+      kk = (int)((a.perm >> (4 * (S % Fd))) & 15) * a.k + 16 * (S / Fd) + 8 * (u & 1);
     } else {
       i = 1 + (g - nc0) / NC;
       kk = 64 * ((g - nc0) % NC) + 8 * u;
@@ -170,13 +179,15 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 
   for (int x = tid; x < kFusedRows * F; x += 256) {
     const int64_t m = m0 + x / F;
-    ids[x] = m < a.B ? clamp_id(a.idx[m * F + x % F], a.M) : 0;
+    const int fe = (int)((a.perm >> (4 * (x % F))) & 15);
+    ids[x] = m < a.B ? clamp_id(a.idx[(a.order ? a.order[m] : m) * F + fe], a.M) : 0;
   }
   for (int i = 0; i < L; ++i)
     for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
   for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
   // Wp: [0, F) the Σw weights, [kFusedMaxF, +k) the FM columns (16-B aligned)
-  for (int x = tid; x < F + k; x += 256) wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x];
+  for (int x = tid; x < F + k; x += 256)
+    wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x < F ? (int)((a.perm >> (4 * x)) & 15) : x];
   int* plo = reinterpret_cast<int*>(smem + kPlo);   // [0,16) lo, [16,32) hi, [32,48) LDS base
   if (PROJ && tid < kFusedMaxF) {
     plo[tid] = 0x7fffffff;
@@ -591,7 +602,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     if (h == 0 && m < a.B) {
       float y1 = 0.f;
       for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
-      a.out[m] = ((y1 + y2) + a.bp) + part;
+      a.out[a.order ? a.order[m] : m] = ((y1 + y2) + a.bp) + part;
     }
   };
   if constexpr (PROJ) {
@@ -934,15 +945,16 @@ bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims) {
 
 int dfm_proj_ld(int L, const int32_t* dims) { return 32 * fused_tm(fused_max_tiles(L, dims)); }
 
-// P for the projected fields [proj_from, F)
+// P for the projected (internal) fields [proj_from, F): P_j = W0 restricted to
+// the caller's field perm(j)
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims) {
   const size_t p = (size_t)(F - proj_from) * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
   return ((p + 255) & ~size_t(255)) + (((size_t)M * 4 + 255) & ~size_t(255));
 }
 
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
-                        int proj_from, const void* Wt0, int N0, int L, const int32_t* dims,
-                        void* ws, hipStream_t st) {
+                        int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
+                        const int32_t* dims, void* ws, hipStream_t st) {
   const int ld = dfm_proj_ld(L, dims);
   const size_t esz = mlp_bf16 ? 2 : 4;   // weight element size
   const size_t pbytes = ((size_t)(F - proj_from) * M * ld * 4 + 255) & ~size_t(255);
@@ -956,7 +968,7 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
     g.N = N0;
     g.K = k;
     g.gidx = iota; g.T = E; g.Mtab = M; g.F = 1; g.kf = k; g.t_bf16 = tbf;
-    g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)f * k * esz;
+    g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)((perm >> (4 * f)) & 15) * k * esz;
     g.ldb = ldb0;
     g.relu = 0;
     g.C = reinterpret_cast<float*>(ws) + (size_t)(f - proj_from) * M * ld;
@@ -974,7 +986,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      hipStream_t st) {
+                      uint64_t perm, const int32_t* order, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -997,9 +1009,12 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.proj_fstride = (int64_t)M * a.proj_ld;
   const bool pj = proj != nullptr;
   a.Fd = pj ? proj_from : F;
+  a.perm = perm;
+  a.order = order;
   if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
-    if (pj && proj_from != 0) return false;   // the fp32 kernel projects all fields
+    // the fp32 kernel projects all fields, in the caller's order
+    if ((pj && proj_from != 0) || perm != kDfmIdentityPerm || order) return false;
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
     const int nc0 = pj ? 0 : (F * (k / 16) + 1) / 2;
     const int64_t units = (int64_t)(nc0 + (L - 1) * TM) * 32 * TM * 8;
@@ -1059,6 +1074,61 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   }
 #undef HHFM_FUSED
   return true;
+}
+
+// ---------------------------------------------------------------------------
+// Row grouping for the projected kernel: a stable radix sort of the row
+// indices by one field's id (hipCUB), so a 128-row block sees few distinct
+// ids of that field and its P rows stage in LDS.  Scores are written back to
+// the caller's row positions; every row's arithmetic is unchanged.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dfm_order_keys(const int32_t* __restrict__ idx,
+                                                      int64_t B, int F, int key_field, int64_t M,
+                                                      uint32_t* __restrict__ keys,
+                                                      int32_t* __restrict__ vals) {
+  for (int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; m < B;
+       m += (int64_t)gridDim.x * blockDim.x) {
+    keys[m] = (uint32_t)clamp_id(idx[m * F + key_field], M);
+    vals[m] = (int32_t)m;
+  }
+}
+
+static int dfm_key_bits(int64_t M) {
+  int b = 1;
+  while (b < 31 && (int64_t(1) << b) < M) ++b;
+  return b;
+}
+
+static size_t dfm_al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+size_t dfm_order_bytes(int64_t B, int64_t M) {
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr,
+                                           (uint32_t*)nullptr, (const int32_t*)nullptr,
+                                           (int32_t*)nullptr, (int)B, 0, dfm_key_bits(M));
+  return 4 * dfm_al256((size_t)B * 4) + dfm_al256(tmp);
+}
+
+// returns the row order (in ws), or null when B does not fit the sort's int
+const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
+                              void* ws, hipStream_t st) {
+  if (B < 1 || B > 0x7fffffff) return nullptr;
+  char* p = reinterpret_cast<char*>(ws);
+  const size_t col = dfm_al256((size_t)B * 4);
+  uint32_t* kin = reinterpret_cast<uint32_t*>(p);
+  uint32_t* kout = reinterpret_cast<uint32_t*>(p + col);
+  int32_t* vin = reinterpret_cast<int32_t*>(p + 2 * col);
+  int32_t* vout = reinterpret_cast<int32_t*>(p + 3 * col);
+  size_t tmp = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)B, 0,
+                                           dfm_key_bits(M), st);
+  const int64_t nb = (B + 255) / 256 < 8192 ? (B + 255) / 256 : 8192;
+  hipLaunchKernelGGL(dfm_order_keys, dim3((unsigned)nb), dim3(256), 0, st, idx, B, F, key_field,
+                     M, kin, vin);
+  if (hipcub::DeviceRadixSort::SortPairs(p + 4 * col, tmp, kin, kout, vin, vout, (int)B, 0,
+                                         dfm_key_bits(M), st) != hipSuccess)
+    return nullptr;
+  return vout;
 }
 
 }  // namespace hhfm

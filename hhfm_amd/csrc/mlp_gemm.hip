@@ -30,12 +30,16 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      hipStream_t st);
+                      uint64_t perm, const int32_t* order, hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
-                        int proj_from, const void* Wt0, int N0, int L, const int32_t* dims,
-                        void* ws, hipStream_t st);
+                        int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
+                        const int32_t* dims, void* ws, hipStream_t st);
+size_t dfm_order_bytes(int64_t B, int64_t M);
+const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
+                              void* ws, hipStream_t st);
+constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
 
 // ---------------------------------------------------------------------------
 // FM part of DeepFM and the final reduce
@@ -102,12 +106,14 @@ __global__ __launch_bounds__(256) void dfm_build_rows(const int32_t* __restrict_
 
 // workspace: [base B][partial B*ntiles][h0 B*maxL][h1 B*maxL][packed weights of
 // the fused kernels, when their envelope admits the layer widths][projected
-// layer 0 (dfm_fused.hip), when planned]
+// layer 0 (dfm_fused.hip), when planned][row order, when planned]
 struct DfmPlan {
-  size_t off_base, off_part, off_h0, off_h1, off_pack, off_proj, total;
+  size_t off_base, off_part, off_h0, off_h1, off_pack, off_proj, off_order, total;
   int maxL, ntl;
   bool proj;
-  int proj_from;   // first projected field (fields [proj_from, F) come from P)
+  int proj_from;   // internal fields [proj_from, F) come from P
+  uint64_t perm;   // internal field j = caller's field (perm >> 4j) & 15
+  bool group;      // rows grouped by the caller's field perm(proj_from) (forward)
 };
 
 static size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -118,19 +124,23 @@ static int pad8(int x) { return (x + 7) & ~7; }
 constexpr size_t kProjMaxBytes = size_t(1) << 30;
 
 // proj_mode (include/hhfm.h hhfm_dfm_proj): OFF plans no projection (F, k,
-// M unused); ON projects every field, CTX the fields >= 2 (LoadData's
-// contexts after user and item; bf16 MLP only) whenever the fused kernels
-// admit the shape and P fits kProjMaxBytes; AUTO picks ON for the fp32 MLP
-// when rows_total >= 2·M (P costs one layer-0 row per table row and field)
-// and CTX for the bf16 MLP under the same condition with F >= 3.  With the
-// bf16 MLP projecting every field is not a win — the user and item rows of P
-// are table-random fp32 rows, more bytes per row than the weight stream they
-// replace (C5 L3, bf16 table: 4.83 ms projected vs 4.51 direct per 2 M rows)
-// — while the context fields' P rows are few and cache-resident (CTX: 3.98
-// ms, -12 %; with an fp32 table +1.6 %, profiles/r02_dfm_ctx_phases.json).
+// M unused); ON projects every field; CTX the fields >= 2 (LoadData's
+// contexts after user and item; bf16 MLP); ITEM every field but the item
+// (bf16 MLP; the item is field 1 of a forward row, item_col of a catalog row)
+// with the forward's rows grouped by field 0, so a block's user P rows stage
+// in LDS like the contexts' (a catalog block is one query already) — each
+// whenever the fused kernels admit the shape and P fits kProjMaxBytes.
+// AUTO: nothing below rows_total = 2·M (P costs one layer-0 row per table
+// row and projected field); ON for the fp32 MLP; for the bf16 MLP ITEM in
+// the catalog, and in the forward once rows_total >= 64·M (grouping pays
+// when a user has many rows), CTX below that.  Projecting the user and item
+// fields straight from HBM is not a win with the bf16 MLP: their P rows are
+// table-random fp32 rows, more bytes per row than the weight stream they
+// replace (profiles/r02_dfm_ctx_phases.json).
 static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype, int F = 0,
                         int k = 0, int64_t M = 0, int64_t rows_total = 0,
-                        int proj_mode = HHFM_DFM_PROJ_OFF) {
+                        int proj_mode = HHFM_DFM_PROJ_OFF, int item_field = 1,
+                        bool forward = true) {
   DfmPlan p{};
   p.maxL = 0;
   for (int i = 0; i < nlayers; ++i) p.maxL = pad8(dims[i]) > p.maxL ? pad8(dims[i]) : p.maxL;
@@ -146,30 +156,47 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
     off += al256(dfm_fused_pack_bytes(nlayers, dims, mlp_dtype == HHFM_BF16));
   p.off_proj = off;
   p.proj_from = -1;
+  p.perm = kDfmIdentityPerm;
+  const bool bf = mlp_dtype == HHFM_BF16;
   int mode = proj_mode;
   if (mode == HHFM_DFM_PROJ_AUTO)
     mode = rows_total < 2 * M ? HHFM_DFM_PROJ_OFF
-           : mlp_dtype == HHFM_F32 ? HHFM_DFM_PROJ_ON
+           : !bf ? HHFM_DFM_PROJ_ON
+           : (!forward || rows_total >= 64 * M) ? HHFM_DFM_PROJ_ITEM
            : HHFM_DFM_PROJ_CTX;
   int from = -1;
+  uint64_t perm = kDfmIdentityPerm;
   if (mode == HHFM_DFM_PROJ_ON) from = 0;
-  if (mode == HHFM_DFM_PROJ_CTX && mlp_dtype == HHFM_BF16 && F >= 3) from = 2;
-  if (from == 2 && getenv("HHFM_EXP_FROM")) from = atoi(getenv("HHFM_EXP_FROM"));  // EXPERIMENT
+  if (mode == HHFM_DFM_PROJ_CTX && bf && F >= 3) from = 2;
+  if (mode == HHFM_DFM_PROJ_ITEM && bf && F >= 2 && item_field >= 0 && item_field < F) {
+    from = 1;
+    perm = (uint64_t)item_field;   // the item first, then the others in order
+    for (int f = 0, j = 1; f < F; ++f)
+      if (f != item_field) perm |= (uint64_t)f << (4 * j++);
+    for (int j = F; j < 16; ++j) perm |= (uint64_t)j << (4 * j);
+  }
   if (from >= 0 && M > 0 && dfm_proj_eligible(F, k, nlayers, dims)) {
     const size_t pb = dfm_proj_bytes(F, from, M, nlayers, dims);
     if (pb <= kProjMaxBytes) {
       p.proj = true;
       p.proj_from = from;
+      p.perm = perm;
       off += al256(pb);
+      p.off_order = off;
+      if (mode == HHFM_DFM_PROJ_ITEM && forward && B <= 0x7fffffff) {
+        p.group = true;
+        off += al256(dfm_order_bytes(B, M));
+      }
     }
   }
+  if (!p.group) p.off_order = off;
   p.total = off;
   return p;
 }
 
 static bool proj_mode_ok(int m) {
   return m == HHFM_DFM_PROJ_OFF || m == HHFM_DFM_PROJ_ON || m == HHFM_DFM_PROJ_AUTO ||
-         m == HHFM_DFM_PROJ_CTX;
+         m == HHFM_DFM_PROJ_CTX || m == HHFM_DFM_PROJ_ITEM;
 }
 
 static int dfm_check(int64_t B, int32_t F, int32_t k, int32_t dtype, int32_t nlayers,
@@ -191,7 +218,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             int32_t nlayers, const int32_t* dims, const void* const* Wt,
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
                             float bp, float* out, char* ws, const DfmPlan& p, const void* proj,
-                            hipStream_t st) {
+                            const int32_t* order, hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
   // One fused kernel per 128-row block when the shape fits (dfm_fused.hip,
   // bf16 or fp32 MLP); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
@@ -201,7 +228,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
   }();
   if ((proj || !layered) && p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
-                       Wp, bp, out, ws + p.off_pack, proj, p.proj_from, st))
+                       Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order, st))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);
@@ -275,14 +302,18 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
                                int32_t mlp_dtype, const float* Wp, float bp, float* out,
                                char* ws, const DfmPlan& p, hipStream_t st) {
   const void* proj = nullptr;
+  const int32_t* order = nullptr;
   if (p.proj) {
     dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F,
-                       p.proj_from, Wt[0], layer_dims[0], nlayers, layer_dims,
+                       p.proj_from, p.perm, Wt[0], layer_dims[0], nlayers, layer_dims,
                        ws + p.off_proj, st);
     proj = ws + p.off_proj;
+    if (p.group)
+      order = dfm_order_rows(idx, B, F, (int)((p.perm >> (4 * p.proj_from)) & 15), features_M,
+                             ws + p.off_order, st);
   }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
-                          mlp_dtype, Wp, bp, out, ws, p, proj, st);
+                          mlp_dtype, Wp, bp, out, ws, p, proj, order, st);
 }
 
 static int dfm_forward_args(const int32_t* idx, int64_t B, int32_t F, const void* E,
@@ -370,8 +401,9 @@ extern "C" int hhfm_dfm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t 
   if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
+  // (the item column moves no workspace: any column gives the catalog's size)
   const DfmPlan p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                             B * (int64_t)item_count, proj_mode);
+                             B * (int64_t)item_count, proj_mode, 1, false);
   *ws_bytes = dfm_cat_bytes(p, rows, F);
   return HHFM_OK;
 }
@@ -398,12 +430,12 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
   DfmPlan p;
   if (proj_mode < 0) {   // legacy entry point: every field projected when the workspace holds it
     p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                 B * (int64_t)item_count, HHFM_DFM_PROJ_ON);
+                 B * (int64_t)item_count, HHFM_DFM_PROJ_ON, item_col, false);
     if (!p.proj || !workspace || ws_bytes < dfm_cat_bytes(p, rows, F))
       p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
   } else {
     p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                 B * (int64_t)item_count, proj_mode);
+                 B * (int64_t)item_count, proj_mode, item_col, false);
   }
   if (!workspace || ws_bytes < dfm_cat_bytes(p, rows, F)) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
@@ -413,7 +445,7 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
   const void* proj = nullptr;
   if (p.proj) {   // once per call: every query chunk reuses it
     dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F,
-                       p.proj_from, Wt[0], layer_dims[0], nlayers, layer_dims,
+                       p.proj_from, p.perm, Wt[0], layer_dims[0], nlayers, layer_dims,
                        ws + p.off_proj, st);
     proj = ws + p.off_proj;
   }
@@ -425,7 +457,7 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
     hipLaunchKernelGGL(dfm_build_rows, dim3((unsigned)blocks), dim3(256), 0, st, qidx + b0 * F,
                        nb, F, item_col, item_row_begin, item_count, rbuf);
     rc = dfm_forward_impl(rbuf, nrows, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
-                          bias, mlp_dtype, Wp, bp, sc, ws, p, proj, st);
+                          bias, mlp_dtype, Wp, bp, sc, ws, p, proj, nullptr, st);
     if (rc) return rc;
     launch_topk_dense(sc, nb, item_count, item_count, K, global_item_base, top_score + b0 * K,
                       top_idx + b0 * K, st);

@@ -214,8 +214,9 @@ def dfm_prepare_weights(layers, biases, mlp_dtype: torch.dtype, F: int, k: int):
     return Wt, bs, dims
 
 
-# include/hhfm.h hhfm_dfm_proj: off / on / auto / context fields only
-DFM_PROJ = {False: 0, True: 1, None: 2, "ctx": 3}
+# include/hhfm.h hhfm_dfm_proj: off / on / auto / context fields only / every
+# field but the item
+DFM_PROJ = {False: 0, True: 1, None: 2, "ctx": 3, "item": 4}
 
 
 def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
@@ -225,8 +226,9 @@ def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, d
     """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B].
 
     ``proj``: projected layer 0 (include/hhfm.h, ABI v3) — None lets the
-    library decide (rows >= 2 x table rows), True / False force it on / off,
-    "ctx" projects the context fields 2..F-1 only (bf16 MLP)."""
+    library decide (include/hhfm.h HHFM_DFM_PROJ_AUTO), True / False force it
+    on / off, "ctx" projects the context fields 2..F-1 only and "item" every
+    field but the item (bf16 MLP)."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, Wp, *Wt, *bias)
     B, F = idx.shape

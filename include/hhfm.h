@@ -192,12 +192,20 @@ int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_
 enum hhfm_dfm_proj {
   HHFM_DFM_PROJ_OFF = 0,  /* plan the direct path only                       */
   HHFM_DFM_PROJ_ON = 1,   /* project every field                             */
-  HHFM_DFM_PROJ_AUTO = 2, /* when rows (B, or B·item_count) >= 2·M: ON for
-                             the fp32 MLP, CTX for the bf16 MLP             */
-  HHFM_DFM_PROJ_CTX = 3   /* bf16 MLP, F >= 3: project the context fields
+  HHFM_DFM_PROJ_AUTO = 2, /* below rows (B, or B·item_count) = 2·M: OFF;
+                             fp32 MLP: ON; bf16 MLP: ITEM in the catalog,
+                             ITEM in the forward from rows >= 64·M, CTX
+                             below that                                      */
+  HHFM_DFM_PROJ_CTX = 3,  /* bf16 MLP, F >= 3: project the context fields
                              2..F-1 (LoadData's layout: user, item,
                              contexts), fields 0 and 1 stay on MFMA; other
                              shapes run direct                               */
+  HHFM_DFM_PROJ_ITEM = 4  /* bf16 MLP, F >= 2: project every field but the
+                             item (field 1 of a forward row, item_col of a
+                             catalog row), which stays on MFMA; the forward
+                             processes its rows grouped by field 0 (a device
+                             radix sort; scores land at the caller's row
+                             positions); other shapes run direct             */
 };
 int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k, int64_t features_M,
                                   int32_t nlayers, const int32_t* layer_dims,

@@ -40,6 +40,8 @@ for c in (7, 2, 3):
     cols.append(torch.randint(off, off + c, (B,), generator=g, device=dev))
     off += c
 X = torch.stack(cols, 1).to(torch.int32).contiguous()
+if os.environ.get("PH_SORTSWAP"):   # experiment: rows grouped by user, item as field 0
+    X = X[torch.argsort(X[:, 0], stable=True)][:, [1, 0, 2, 3, 4]].contiguous()
 res = {}
 for mdt in (torch.bfloat16,):
     for tdt in [torch.float32, torch.bfloat16][int(os.environ.get("PH_T0", 0)):]:
@@ -49,10 +51,10 @@ for mdt in (torch.bfloat16,):
             m.validate = False
             Wt, bs, dims, Wp, bp = m._prepared()
             out = torch.empty(B, device=dev)
-            for pj in (False, True, "ctx"):
+            for pj in (False, True, "ctx", "item"):
                 fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1),  # noqa
                                              Wt, bs, dims, mdt, Wp, bp, out=out, proj=pj)
-                key = f"{'bf16' if mdt == torch.bfloat16 else 'f32'}mlp_{'tbf16' if tdt == torch.bfloat16 else 'tf32'}_L{len(layers)}_{ {False: 'direct', True: 'proj', 'ctx': 'ctx'}[pj] }"
+                key = f"{'bf16' if mdt == torch.bfloat16 else 'f32'}mlp_{'tbf16' if tdt == torch.bfloat16 else 'tf32'}_L{len(layers)}_{ {False: 'direct', True: 'proj', 'ctx': 'ctx', 'item': 'item'}[pj] }"
                 res[key] = round(timeit(fn), 4)
             del m
             torch.cuda.empty_cache()

@@ -162,8 +162,9 @@ def test_wide_ids_are_checked_before_narrowing():
 
 def test_dfm_projection_auto_plan():
     """ABI v3 planning: AUTO plans P exactly when rows >= 2 x table rows —
-    every field for the fp32 MLP (ON's workspace), the context fields for the
-    bf16 MLP (CTX's); ON plans every field for both."""
+    every field for the fp32 MLP (ON's workspace); for the bf16 MLP the
+    context fields (CTX) and, from 64 x table rows in the forward or always in
+    the catalog, every field but the item (ITEM); ON plans every field."""
     from hhfm_amd._native import native
     nat = native()
     dims = [400, 400, 400]
@@ -173,7 +174,12 @@ def test_dfm_projection_auto_plan():
         assert on - off >= 5 * 5051 * 416 * 4   # fp32 P
         auto = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 2)
         ctx = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 3)
-        assert auto == (on if md == 0 else ctx) and (md == 0 or off < ctx < on)
+        item = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, md, 4)
+        # 1 M rows >= 64 x 5051: the bf16 forward's AUTO is ITEM; 200 k rows: CTX
+        assert auto == (on if md == 0 else item) and (md == 0 or off < ctx < on)
+        if md == 1:
+            assert (nat.dfm_forward_workspace_ex(200000, 5, 256, 5051, dims, md, 2)
+                    == nat.dfm_forward_workspace_ex(200000, 5, 256, 5051, dims, md, 3))
         small = nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 2)
         assert small == nat.dfm_forward_workspace_ex(10000, 5, 256, 5051, dims, md, 0)
         assert off == nat.dfm_forward_workspace(1 << 20, dims, md)
@@ -186,8 +192,18 @@ def test_dfm_projection_auto_plan():
             == nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 0, 0))
     assert (nat.dfm_forward_workspace_ex(1 << 20, 2, 256, 5051, dims, 1, 3)
             == nat.dfm_forward_workspace_ex(1 << 20, 2, 256, 5051, dims, 1, 0))
+    # ITEM: P for F-1 fields, plus the row-grouping sort's buffers (forward)
+    item = nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 4)
+    assert item - off >= 4 * 5051 * 416 * 4 + 4 * (1 << 20) * 4
+    assert (nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 0, 4)
+            == nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 0, 0))
+    cat_item = nat.dfm_catalog_topk_workspace_ex(100, 5, 256, 5051, 4082, dims, 1, 1 << 20, 4)
+    cat_off = nat.dfm_catalog_topk_workspace_ex(100, 5, 256, 5051, 4082, dims, 1, 1 << 20, 0)
+    assert 4 * 5051 * 416 * 4 <= cat_item - cat_off < 5 * 5051 * 416 * 4
+    assert nat.dfm_catalog_topk_workspace_ex(100, 5, 256, 5051, 4082, dims, 1, 1 << 20,
+                                             2) == cat_item
     with pytest.raises(ValueError):
-        nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 4)
+        nat.dfm_forward_workspace_ex(1 << 20, 5, 256, 5051, dims, 1, 5)
     # outside the fused envelope (k % 16 != 0) nothing is planned
     assert (nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 1)
             == nat.dfm_forward_workspace_ex(1 << 20, 5, 40, 5051, dims, 1, 0))

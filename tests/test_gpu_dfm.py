@@ -107,7 +107,7 @@ def test_dfm_forward_shapes(mlp, k, layers):
         assert np.all(np.abs(got - ref) <= 5e-3 * mag)
 
 
-@pytest.mark.parametrize("proj", [False, True, "ctx"])
+@pytest.mark.parametrize("proj", [False, True, "ctx", "item"])
 @pytest.mark.parametrize("mlp", ["f32", "bf16"])
 def test_dfm_catalog_topk_chunked(mlp, proj):
     """Query chunking (chunk_rows < B*N) gives the same top-K as one pass
@@ -198,11 +198,13 @@ def test_dfm_fused_envelope(F, k, layers, tdt, B, mlp):
     (3, 48, [64, 96, 33, 20], "f32", 1000),     # 4 layers, odd widths
     (11, 32, [128, 416], "bf16", 1),            # widest envelope, one row
 ])
-@pytest.mark.parametrize("mlp,proj", [("bf16", True), ("f32", True), ("bf16", "ctx")])
+@pytest.mark.parametrize("mlp,proj", [("bf16", True), ("f32", True), ("bf16", "ctx"),
+                                      ("bf16", "item")])
 def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
     """Projected layer 0 (h_0 = Σ_f P_f[x_f], dfm_fused.hip PROJ kernels),
-    forced on for every field (True) or for the context fields 2..F-1 with
-    fields 0, 1 on MFMA ("ctx", bf16 MLP), against the same oracles and
+    forced on for every field (True), for the context fields 2..F-1 with
+    fields 0, 1 on MFMA ("ctx", bf16 MLP) or for every field but the item
+    with the rows grouped by user ("item", bf16 MLP), against the same oracles and
     tolerances as the direct kernels, and against the direct kernel itself
     (bf16: summation order only, so the two differ by at most a bf16 flip of
     a hidden unit)."""
@@ -213,7 +215,9 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
     mdt = torch.bfloat16 if mlp == "bf16" else torch.float32
     m = _model((100, 200, M, F, k, layers), mlp_dtype=mdt, table_dtype=tdtype)
     X = rng.integers(0, M, size=(B, F)).astype(np.int32)
-    if proj == "ctx" and F >= 5:
+    if proj == "item":
+        X[:, 0] %= 40   # ~B/40 rows per user: grouped rows stage the user's P rows
+    if proj in ("ctx", "item") and F >= 5:
         # narrow context fields; field 4 narrow in the first half of the rows
         # only: those blocks run LDS-staged (PJ = 2), the rest from HBM
         X[:, 2] = 900 + X[:, 2] % 7
