@@ -77,18 +77,19 @@ struct FusedDfmArgs {
   float bp;
   float* out;
   const uint4* packed;   // chunk sequence written by dfm_pack_weights
-  // PROJ: fp32 P_f[id] at proj + f·proj_fstride + id·proj_ld, zero beyond
+  // PROJ: fp32 P_f[id] at proj + f·proj_fstride + id·proj_ld (f counted from
+  // the first projected field), zero beyond
   // dims[0]; fp32 MLP: natural unit order; bf16 MLP: the accumulator order of
   // dfm_proj_pos (a lane's 16 units of a tile are contiguous)
   const void* proj;
   int64_t proj_fstride;
-  int proj_ld;           // 32·TM
+  int proj_ld;           // row stride: projected fields x 32·TM
   int Fd;                // fields [0, Fd) run layer 0 on MFMA, [Fd, F) come from P
                          // (Fd = F: no projection; 0: all fields projected)
   // bf16 kernel: internal field j is the caller's field (perm >> 4j) & 15
-  // (direct fields first), and block row m is the caller's row order[m]
-  // (rows grouped so that a projected field's ids stage in LDS); order may be
-  // null.  The fp32 kernel takes the identity.
+  // (direct fields first); row m's score goes to out[order[m]] when order is
+  // set (idx then holds the caller's rows regrouped, dfm_order_rows).  The
+  // fp32 kernel takes the identity and no order.
   uint64_t perm;
   const int32_t* order;
 };
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   for (int x = tid; x < kFusedRows * F; x += 256) {
     const int64_t m = m0 + x / F;
     const int fe = (int)((a.perm >> (4 * (x % F))) & 15);
-    ids[x] = m < a.B ? clamp_id(a.idx[(a.order ? a.order[m] : m) * F + fe], a.M) : 0;
+    ids[x] = m < a.B ? clamp_id(a.idx[m * F + fe], a.M) : 0;
   }
   for (int i = 0; i < L; ++i)
     for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
@@ -945,37 +946,65 @@ bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims) {
 
 int dfm_proj_ld(int L, const int32_t* dims) { return 32 * fused_tm(fused_max_tiles(L, dims)); }
 
-// P for the projected (internal) fields [proj_from, F): P_j = W0 restricted to
-// the caller's field perm(j)
+// P for the projected (internal) fields j in [proj_from, F): P_j = W0
+// restricted to the caller's field perm(j), laid out [id][j][NR] (one row of
+// all projected fields per table row), computed by ONE GEMM against the
+// stacked weights Wc[(j, n)][k] = W0[n][perm(j)·k ..] (zero for n >= N0).
+static size_t proj_al(size_t x) { return (x + 255) & ~size_t(255); }
+
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims) {
-  const size_t p = (size_t)(F - proj_from) * (size_t)M * (size_t)dfm_proj_ld(L, dims) * 4;
-  return ((p + 255) & ~size_t(255)) + (((size_t)M * 4 + 255) & ~size_t(255));
+  const size_t ld = (size_t)dfm_proj_ld(L, dims), nf = (size_t)(F - proj_from);
+  return proj_al(nf * (size_t)M * ld * 4) + proj_al((size_t)M * 4) +
+         proj_al(nf * ld * kFusedMaxK * 4);
+}
+
+// Wc rows (j, n), 16-B units: W0 (esz-byte elements, row stride ldb0)
+__global__ __launch_bounds__(256) void dfm_proj_weights(const char* __restrict__ W0, int esz,
+                                                        int ldb0, int N0, int NR, int nf,
+                                                        int proj_from, uint64_t perm, int k,
+                                                        uint4* __restrict__ Wc) {
+  const int upr = k * esz / 16;   // units per row
+  const int64_t total = (int64_t)nf * NR * upr;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = x / upr;
+    const int u = (int)(x - row * upr);
+    const int j = (int)(row / NR), n = (int)(row - (int64_t)j * NR);
+    const int fe = (int)((perm >> (4 * (proj_from + j))) & 15);
+    Wc[x] = n < N0 ? *reinterpret_cast<const uint4*>(W0 + ((size_t)n * ldb0 + (size_t)fe * k) * esz +
+                                                    16 * u)
+                   : make_uint4(0, 0, 0, 0);
+  }
 }
 
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
                         int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
                         const int32_t* dims, void* ws, hipStream_t st) {
-  const int ld = dfm_proj_ld(L, dims);
-  const size_t esz = mlp_bf16 ? 2 : 4;   // weight element size
-  const size_t pbytes = ((size_t)(F - proj_from) * M * ld * 4 + 255) & ~size_t(255);
-  int32_t* iota = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ws) + pbytes);
+  const int ld = dfm_proj_ld(L, dims), nf = F - proj_from;
+  const int esz = mlp_bf16 ? 2 : 4;   // weight element size
+  char* base = reinterpret_cast<char*>(ws);
+  const size_t pbytes = proj_al((size_t)nf * M * ld * 4);
+  int32_t* iota = reinterpret_cast<int32_t*>(base + pbytes);
+  uint4* Wc = reinterpret_cast<uint4*>(base + pbytes + proj_al((size_t)M * 4));
   const int64_t ib = (M + 255) / 256 < 4096 ? (M + 255) / 256 : 4096;
   hipLaunchKernelGGL(dfm_iota, dim3((unsigned)ib), dim3(256), 0, st, iota, M);
-  const int ldb0 = (F * k + 7) & ~7;
-  for (int f = proj_from; f < F; ++f) {
-    GemmArgs g{};
-    g.M = M;
-    g.N = N0;
-    g.K = k;
-    g.gidx = iota; g.T = E; g.Mtab = M; g.F = 1; g.kf = k; g.t_bf16 = tbf;
-    g.Bt = reinterpret_cast<const char*>(Wt0) + (size_t)((perm >> (4 * f)) & 15) * k * esz;
-    g.ldb = ldb0;
-    g.relu = 0;
-    g.C = reinterpret_cast<float*>(ws) + (size_t)(f - proj_from) * M * ld;
-    g.ldc = ld;
-    g.c_perm32 = mlp_bf16;   // the bf16 kernel's accumulator order
-    launch_gemm(g, mlp_bf16, 0, st);
-  }
+  const int64_t wu = (int64_t)nf * ld * (k * esz / 16);
+  hipLaunchKernelGGL(dfm_proj_weights, dim3((unsigned)((wu + 255) / 256 < 2048 ? (wu + 255) / 256
+                                                                               : 2048)),
+                     dim3(256), 0, st, reinterpret_cast<const char*>(Wt0), esz,
+                     (F * k + 7) & ~7, N0, ld, nf, proj_from, perm, k, Wc);
+  GemmArgs g{};
+  g.M = M;
+  g.N = nf * ld;
+  g.K = k;
+  g.gidx = iota; g.T = E; g.Mtab = M; g.F = 1; g.kf = k; g.t_bf16 = tbf;
+  g.Bt = Wc;
+  g.ldb = k;
+  g.relu = 0;
+  g.C = reinterpret_cast<float*>(ws);
+  g.ldc = nf * ld;
+  g.c_perm32 = mlp_bf16;   // the bf16 kernel's accumulator order (ld % 32 == 0)
+  launch_gemm(g, mlp_bf16, 0, st);
 }
 
 // returns false when the shape is outside the fused kernel's envelope.
@@ -1005,8 +1034,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.Wp = Wp; a.bp = bp; a.out = out;
   a.packed = reinterpret_cast<const uint4*>(pack_ws);
   a.proj = proj;
-  a.proj_ld = 32 * TM;
-  a.proj_fstride = (int64_t)M * a.proj_ld;
+  a.proj_fstride = 32 * TM;   // [id][projected field][32·TM] (dfm_project_layer0)
+  a.proj_ld = (proj ? F - proj_from : 1) * 32 * TM;
   const bool pj = proj != nullptr;
   a.Fd = pj ? proj_from : F;
   a.perm = perm;
@@ -1101,20 +1130,36 @@ static int dfm_key_bits(int64_t M) {
 
 static size_t dfm_al256(size_t x) { return (x + 255) & ~size_t(255); }
 
-size_t dfm_order_bytes(int64_t B, int64_t M) {
+// rows[m] = idx[order[m]]: the fused kernel then reads a block's rows as one
+// contiguous slab
+__global__ __launch_bounds__(256) void dfm_gather_rows(const int32_t* __restrict__ idx,
+                                                       const int32_t* __restrict__ order,
+                                                       int64_t B, int F,
+                                                       int32_t* __restrict__ rows) {
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < B * F;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = x / F;
+    rows[x] = idx[(int64_t)order[m] * F + (x - m * F)];
+  }
+}
+
+size_t dfm_order_bytes(int64_t B, int F, int64_t M) {
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr,
                                            (uint32_t*)nullptr, (const int32_t*)nullptr,
                                            (int32_t*)nullptr, (int)B, 0, dfm_key_bits(M));
-  return 4 * dfm_al256((size_t)B * 4) + dfm_al256(tmp);
+  return 4 * dfm_al256((size_t)B * 4) + dfm_al256((size_t)B * F * 4) + dfm_al256(tmp);
 }
 
-// returns the row order (in ws), or null when B does not fit the sort's int
+// Sorts the rows by field key_field: returns the order (in ws) and the
+// regrouped rows in *rows_out, or null when B does not fit the sort's int.
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
-                              void* ws, hipStream_t st) {
+                              void* ws, const int32_t** rows_out, hipStream_t st) {
   if (B < 1 || B > 0x7fffffff) return nullptr;
   char* p = reinterpret_cast<char*>(ws);
   const size_t col = dfm_al256((size_t)B * 4);
+  int32_t* rows = reinterpret_cast<int32_t*>(p + 4 * col);
+  char* tmp_ws = p + 4 * col + dfm_al256((size_t)B * F * 4);
   uint32_t* kin = reinterpret_cast<uint32_t*>(p);
   uint32_t* kout = reinterpret_cast<uint32_t*>(p + col);
   int32_t* vin = reinterpret_cast<int32_t*>(p + 2 * col);
@@ -1125,9 +1170,12 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
   const int64_t nb = (B + 255) / 256 < 8192 ? (B + 255) / 256 : 8192;
   hipLaunchKernelGGL(dfm_order_keys, dim3((unsigned)nb), dim3(256), 0, st, idx, B, F, key_field,
                      M, kin, vin);
-  if (hipcub::DeviceRadixSort::SortPairs(p + 4 * col, tmp, kin, kout, vin, vout, (int)B, 0,
+  if (hipcub::DeviceRadixSort::SortPairs(tmp_ws, tmp, kin, kout, vin, vout, (int)B, 0,
                                          dfm_key_bits(M), st) != hipSuccess)
     return nullptr;
+  const int64_t gb = (B * F + 255) / 256 < 8192 ? (B * F + 255) / 256 : 8192;
+  hipLaunchKernelGGL(dfm_gather_rows, dim3((unsigned)gb), dim3(256), 0, st, idx, vout, B, F, rows);
+  *rows_out = rows;
   return vout;
 }
 

@@ -36,9 +36,9 @@ size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dim
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
                         int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
                         const int32_t* dims, void* ws, hipStream_t st);
-size_t dfm_order_bytes(int64_t B, int64_t M);
+size_t dfm_order_bytes(int64_t B, int F, int64_t M);
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
-                              void* ws, hipStream_t st);
+                              void* ws, const int32_t** rows_out, hipStream_t st);
 constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
 
 // ---------------------------------------------------------------------------
@@ -185,7 +185,7 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
       p.off_order = off;
       if (mode == HHFM_DFM_PROJ_ITEM && forward && B <= 0x7fffffff) {
         p.group = true;
-        off += al256(dfm_order_bytes(B, M));
+        off += al256(dfm_order_bytes(B, F, M));
       }
     }
   }
@@ -308,9 +308,11 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
                        p.proj_from, p.perm, Wt[0], layer_dims[0], nlayers, layer_dims,
                        ws + p.off_proj, st);
     proj = ws + p.off_proj;
+    const int32_t* grouped = nullptr;
     if (p.group)
       order = dfm_order_rows(idx, B, F, (int)((p.perm >> (4 * p.proj_from)) & 15), features_M,
-                             ws + p.off_order, st);
+                             ws + p.off_order, &grouped, st);
+    if (order) idx = grouped;
   }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
                           mlp_dtype, Wp, bp, out, ws, p, proj, order, st);
