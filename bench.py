@@ -390,9 +390,10 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
     """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137),
     Frappe vocabulary, `rows` rows per GPU (12.5M = the 100M-row job over 8
     GPUs; weak scaling, rows sharded, no collective).  mlp=bf16: the fused
-    bf16-MFMA kernel, user and item fields of layer 0 on MFMA, the context
-    fields projected (HHFM_DFM_PROJ_CTX, P computed inside every step); its
-    roofline prices the reference's FLOPs and states the executed ones;
+    bf16-MFMA kernel, the item field of layer 0 on MFMA, the others
+    projected (HHFM_DFM_PROJ_ITEM via AUTO: P and the user grouping computed
+    inside every step); its roofline prices the reference's FLOPs and states
+    the executed ones;
     mlp=fp32 (the reference numerics):
     exact-fp32 MFMA with the projected layer 0 (include/hhfm.h ABI v3: P =
     W0-projection of every table row once per call inside the timed step,
@@ -444,13 +445,15 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
     kern = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     fl = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
     if mlp == torch.bfloat16:
-        # executed: projection of the 12 context rows x 3 fields + fields 0-1
-        # of layer 0 and the hidden layers per row
-        ex = 2.0 * 3 * sum(ctx) * 256 * 400 + rows * (2.0 * (2 * 256 * 400 + 2 * 400 * 400)
-                                                      + 2.0 * (5 + 256 + 400))
+        # executed (AUTO = ITEM): the projection of the M table rows for the 4
+        # non-item fields, then the item field of layer 0 and the hidden
+        # layers per row
+        ex = 2.0 * 4 * M * 256 * 400 + rows * (2.0 * (256 * 400 + 2 * 400 * 400)
+                                               + 2.0 * (5 + 256 + 400))
         return {"workload": "C5 (configs[4]): DeepFM F=5 k=256 + MLP 3x400 (bf16 table as "
-                            "SURVEY §8d prices it, bf16 MFMA, fp32 accumulation and FM part, "
-                            "context fields of layer 0 projected inside every step), "
+                            "SURVEY §8d prices it, bf16 MFMA, fp32 accumulation and FM part; "
+                            "layer 0 of every field but the item projected and the rows "
+                            "grouped by user inside every step), "
                             f"Frappe vocabulary, rows sharded {rows:,} per GPU", "ranks": world,
                 "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
                 "executed_TFLOPs": ex / (kern * 1e-3) / 1e12,

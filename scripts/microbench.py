@@ -107,8 +107,11 @@ if not only or "dfm" in only:
             (torch.float32, torch.float32, "dfm_c5_f32")]
     if os.environ.get("MB_DFM_LEGS"):
         legs = [x for x in legs if x[2] in os.environ["MB_DFM_LEGS"].split(",")]
-    # MB_DFM_PROJ: "0" direct layer 0 only, "1" projected only, default both
-    projs = {"0": [False], "1": [True]}.get(os.environ.get("MB_DFM_PROJ", ""), [False, True])
+    # MB_DFM_PROJ: "0" direct layer 0 only, "1" every field projected only,
+    # "auto" the library's choice only (bf16 MLP: ITEM; fp32 MLP: every field);
+    # default all three
+    projs = {"0": [False], "1": [True], "auto": [None]}.get(os.environ.get("MB_DFM_PROJ", ""),
+                                                             [False, True, None])
     for mdt, tdt, name in legs:
         m = DeepFM(nu, ni, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
                    mlp_dtype=mdt, table_dtype=tdt)
@@ -120,14 +123,16 @@ if not only or "dfm" in only:
             fn = lambda: ops.dfm_forward(X, m.table, m.weights["feature_bias"].reshape(-1),  # noqa
                                          Wt, bs, dims, mdt, Wp, bp, out=out, proj=pj)
             med, mn = timeit(fn, reps=5)
-            leg = name + ("_proj" if pj else "")
+            leg = name + {False: "", True: "_proj", None: "_auto"}[pj]
             res[leg] = {"median_ms": med, "rows_per_s": B / (med * 1e-3),
                         "TFLOPs_reference_flops": flops_row * B / (med * 1e-3) / 1e12}
             outs[pj] = out
-        if len(outs) == 2:
-            d = (outs[True] - outs[False]).abs().max().item()
-            res[name + "_proj"]["max_abs_diff_vs_direct"] = d
-            res[name + "_proj"]["out_abs_max"] = outs[False].abs().max().item()
+        if False in outs:
+            for pj, suf in ((True, "_proj"), (None, "_auto")):
+                if pj in outs:
+                    res[name + suf]["max_abs_diff_vs_direct"] = \
+                        (outs[pj] - outs[False]).abs().max().item()
+                    res[name + suf]["out_abs_max"] = outs[False].abs().max().item()
         del m, outs
         torch.cuda.empty_cache()
 

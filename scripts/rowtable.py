@@ -160,8 +160,9 @@ if not only or "c5" in only:
     X, M = frappe_rows(rng, B)
     Xg = torch.from_numpy(X).to(dev)
     for mdt, name in ((torch.bfloat16, "C5_D1_dfm_bf16_mlp"), (torch.float32, "C5_D1_dfm_fp32_mlp")):
+        # the bf16 MLP reads a bf16 table, as SURVEY §8d prices C5 (and bench.py)
         m = DeepFM(957, 4082, M, 5, 256, [400, 400, 400], None, 0.01, 0, 0.0, device=dev,
-                   mlp_dtype=mdt)
+                   mlp_dtype=mdt, table_dtype=mdt)
         m.validate = False
         Wt, bs, dims, Wp, bp = m._prepared()
         out = torch.empty(B, device=dev)
@@ -178,9 +179,16 @@ if not only or "c5" in only:
                                       Ls, Bs_, W["concat_projection"], float(W["concat_bias"])))
         peak = BF16_TF if mdt == torch.bfloat16 else F32_TF
         if mdt == torch.bfloat16:
+            # AUTO = ITEM: fields other than the item projected (rows grouped by
+            # user), the item field and the hidden layers on MFMA
+            ex = 2.0 * 4 * M * 256 * 400 + nrows * (2.0 * (256 * 400 + 2 * 400 * 400)
+                                                    + 2.0 * (5 + 256 + 400))
             roof = {"bound": "MFMA", "flops_per_unit": fl,
-                    "frac": fl * nrows / (ms * 1e-3) / 1e12 / peak}
-            cfg = f"DFM F=5 k=256 MLP 3x400 (bf16), {nrows:,} rows"
+                    "frac": fl * nrows / (ms * 1e-3) / 1e12 / peak,
+                    "executed_flops_per_unit": ex / nrows,
+                    "executed_frac": ex / (ms * 1e-3) / 1e12 / peak}
+            cfg = (f"DFM F=5 k=256 MLP 3x400 (bf16 MLP and table; AUTO projection = every "
+                   f"field but the item), {nrows:,} rows")
         else:
             # the fp32 MLP runs the projected layer 0 (AUTO: rows >= 2 x table
             # rows): executed FLOPs = the per-call projection of the M table
