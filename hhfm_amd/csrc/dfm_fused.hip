@@ -156,7 +156,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   // PROJ: the rest of the LDS stages P rows of projected fields whose ids in
   // this block span few table rows (row stride NR + 4 floats: rows of distinct
   // ids start 4 banks apart)
-  constexpr int kPst = kPlo + 4 * kFusedMaxF * 4;
+  constexpr int kYl = kPlo + 4 * kFusedMaxF * 4;   // per-row Σ_f w[x_f]·Wp[f]
+  constexpr int kPst = kYl + kFusedRows * 4;
   constexpr int kPsLd = NR + 4;
   constexpr int kPsFloats = PROJ ? (kLdsBytes - kPst) / 4 : 0;
   constexpr int kSmem = kPst + kPsFloats * 4;
@@ -308,6 +309,30 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
       }
     };
 
+    // Everything the block's first MFMA chunk waits for is issued together and
+    // met by ONE barrier: layer-0 chunk 0 (weights + gathered embeddings; with
+    // every field projected, hidden chunk 0), the staged rows, and the Σw
+    // term of the output (one row per thread, all F loads in flight).
+    EChunk e0, e1;
+    Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
+    const bool direct0 = !PROJ || Fd > 0;
+    if (direct0) {
+      eload(e0, cg);
+      dma(0, 0);
+    } else if (nchunks > 0) {
+      dma(0, 0);
+    }
+    float* ylds = reinterpret_cast<float*>(smem + kYl);
+    if (tid < kFusedRows) {
+      float wv8[kFusedMaxF];
+  #pragma unroll
+      for (int f = 0; f < kFusedMaxF; ++f) wv8[f] = f < F ? a.w[ids[tid * F + f]] : 0.f;
+      float y1 = 0.f;
+  #pragma unroll
+      for (int f = 0; f < kFusedMaxF; ++f)
+        if (f < F) y1 += wv8[f] * wpl[f];
+      ylds[tid] = y1;
+    }
     if constexpr (PROJ) {
       // ----- ST: the block's projected fields' P rows and table rows, rows
       // lo..hi of each, staged in LDS (read below instead of HBM) -----
@@ -333,12 +358,15 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
           }
           used += span * (kPsLd + ek);
         }
-        __syncthreads();
       }
+    }
+    __syncthreads();   // vmcnt(0): chunk 0, the staged rows and the Σw terms landed
+    if constexpr (PROJ) {
+      float* pst = reinterpret_cast<float*>(smem + kPst);
+      const float* P = reinterpret_cast<const float*>(a.proj);
       // ----- projected layer 0: acc = Σ_{f >= Fd} P_f[x_f]; with Fd == 0 also
       // the FM part from the table (otherwise the direct loop below adds the
       // MFMA part of fields < Fd and the FM part) -----
-      if (Fd == 0 && nchunks > 0) dma(0, 0);   // hidden chunk 0 streams behind the gathers
       // lane (r, h) holds units 32t + 8g + 4h + e of its row (32x32 C/D map):
       // one float4 of P per (field, tile, g); all 4·TM of a field in flight.
       // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
@@ -346,7 +374,9 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   #ifndef HHFM_KO_PROJP
       for (int f = Fd; f < F; ++f) {
         // P in accumulator order: positions 32t + 16h .. +15 are this lane's
-        // units of tile t (64 contiguous bytes), from LDS when staged
+        // units of tile t (64 contiguous bytes), from LDS when staged; all
+        // 4·TM reads of a field in flight (a tile-outer order, each tile's
+        // fields summed in registers first, ran 6 % slower)
         auto addp = [&](const float4* pp) {
   #pragma unroll
           for (int t = 0; t < TM; ++t)
@@ -410,14 +440,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         y2 += d;
   #endif
       }
-      if (Fd == 0) __syncthreads();   // vmcnt(0): hidden chunk 0 landed
     }
-    if (!PROJ || Fd > 0) {
-    EChunk e0, e1;
-    Cur cg{0, 0, 0}, cs{0, 0, 0};   // next gather step, next FM-side step
-    eload(e0, cg);
-    dma(0, 0);
-    __syncthreads();   // vmcnt(0): chunk 0 in LDS
+    if (direct0) {
 
     // ----- layer 0: B operand = gathered embeddings; FM part on the side -----
     // Chunk c first turns the embeddings gathered during chunk c-1 into its 4
@@ -600,11 +624,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
     part += __shfl_xor(part, 32, kWave);
     y2 += __shfl_xor(y2, 32, kWave);
     const int64_t m = m0 + myrow;
-    if (h == 0 && m < a.B) {
-      float y1 = 0.f;
-      for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
-      a.out[a.order ? a.order[m] : m] = ((y1 + y2) + a.bp) + part;
-    }
+    if (h == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = ((ylds[myrow] + y2) + a.bp) + part;
   };
   if constexpr (PROJ) {
     if (allfit) body(BoolC<true>{});
