@@ -1126,8 +1126,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
 }
 
 // ---------------------------------------------------------------------------
-// Row grouping for the projected kernel: a stable radix sort of the row
-// indices by one field's id (hipCUB), so a 128-row block sees few distinct
+// Row grouping for the projected kernel: the row indices ordered by one
+// field's id (counting sort below, or hipCUB's radix sort), so a 128-row block sees few distinct
 // ids of that field and its P rows stage in LDS.  Scores are written back to
 // the caller's row positions; every row's arithmetic is unchanged.
 // ---------------------------------------------------------------------------
@@ -1163,15 +1163,93 @@ __global__ __launch_bounds__(256) void dfm_gather_rows(const int32_t* __restrict
   }
 }
 
+// Counting-sort grouping for key ranges up to kGroupBins ids (Frappe's users:
+// 957 of 5,051 table rows): every block histograms its slice of rows in LDS,
+// reserves one range per (block, id) with a global atomic, and scatters its
+// rows straight into the grouped copy (and their positions into the order).
+// Positions inside one id's group depend on atomic timing — every row's
+// arithmetic does not, so the scores are identical either way.  Larger key
+// ranges take hipCUB's radix sort.
+constexpr int kGroupBins = 16384;
+constexpr int kGroupRows = 8192;   // rows per block
+
+__global__ __launch_bounds__(256) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
+                                                      int F, int key_field, int64_t M,
+                                                      uint32_t* __restrict__ count) {
+  __shared__ uint32_t hcnt[kGroupBins];
+  const int nb = (int)M;
+  for (int b = threadIdx.x; b < nb; b += 256) hcnt[b] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
+  const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256)
+    atomicAdd(&hcnt[clamp_id(idx[m * F + key_field], M)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += 256)
+    if (hcnt[b]) atomicAdd(&count[b], hcnt[b]);
+}
+
+// exclusive scan of count[0, M) into start (one block)
+__global__ __launch_bounds__(1024) void dfm_group_scan(const uint32_t* __restrict__ count,
+                                                       int64_t M, uint32_t* __restrict__ start) {
+  __shared__ uint32_t part[1024];
+  const int per = (int)((M + 1023) / 1024);
+  const int b0 = threadIdx.x * per;
+  uint32_t s = 0;
+  for (int b = b0; b < b0 + per && b < M; ++b) s += count[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan
+    const uint32_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[threadIdx.x] - s;   // exclusive prefix of this thread's bins
+  for (int b = b0; b < b0 + per && b < M; ++b) {
+    start[b] = run;
+    run += count[b];
+  }
+}
+
+__global__ __launch_bounds__(256) void dfm_group_scatter(const int32_t* __restrict__ idx,
+                                                         int64_t B, int F, int key_field,
+                                                         int64_t M,
+                                                         const uint32_t* __restrict__ start,
+                                                         uint32_t* __restrict__ cursor,
+                                                         int32_t* __restrict__ rows,
+                                                         int32_t* __restrict__ order) {
+  __shared__ uint32_t hpos[kGroupBins];
+  const int nb = (int)M;
+  for (int b = threadIdx.x; b < nb; b += 256) hpos[b] = 0;
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
+  const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256)
+    atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += 256)   // this block's range inside id b's group
+    if (hpos[b]) hpos[b] = start[b] + atomicAdd(&cursor[b], hpos[b]);
+  __syncthreads();
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256) {
+    const uint32_t pos = atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
+    for (int f = 0; f < F; ++f) rows[(int64_t)pos * F + f] = idx[m * F + f];
+    order[pos] = (int32_t)m;
+  }
+}
+
 size_t dfm_order_bytes(int64_t B, int F, int64_t M) {
   size_t tmp = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr,
-                                           (uint32_t*)nullptr, (const int32_t*)nullptr,
-                                           (int32_t*)nullptr, (int)B, 0, dfm_key_bits(M));
+  if (M > kGroupBins)
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, (const uint32_t*)nullptr,
+                                             (uint32_t*)nullptr, (const int32_t*)nullptr,
+                                             (int32_t*)nullptr, (int)B, 0, dfm_key_bits(M));
+  else
+    tmp = 3 * dfm_al256((size_t)M * 4);
   return 4 * dfm_al256((size_t)B * 4) + dfm_al256((size_t)B * F * 4) + dfm_al256(tmp);
 }
 
-// Sorts the rows by field key_field: returns the order (in ws) and the
+// Groups the rows by field key_field: returns the order (in ws) and the
 // regrouped rows in *rows_out, or null when B does not fit the sort's int.
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
                               void* ws, const int32_t** rows_out, hipStream_t st) {
@@ -1180,10 +1258,25 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
   const size_t col = dfm_al256((size_t)B * 4);
   int32_t* rows = reinterpret_cast<int32_t*>(p + 4 * col);
   char* tmp_ws = p + 4 * col + dfm_al256((size_t)B * F * 4);
+  int32_t* vout = reinterpret_cast<int32_t*>(p + 3 * col);
+  if (M <= kGroupBins) {
+    const size_t mb = dfm_al256((size_t)M * 4);
+    uint32_t* count = reinterpret_cast<uint32_t*>(tmp_ws);
+    uint32_t* cursor = reinterpret_cast<uint32_t*>(tmp_ws + mb);
+    uint32_t* start = reinterpret_cast<uint32_t*>(tmp_ws + 2 * mb);
+    if (hipMemsetAsync(count, 0, 2 * mb, st) != hipSuccess) return nullptr;
+    const unsigned nblk = (unsigned)((B + kGroupRows - 1) / kGroupRows);
+    hipLaunchKernelGGL(dfm_group_hist, dim3(nblk), dim3(256), 0, st, idx, B, F, key_field, M,
+                       count);
+    hipLaunchKernelGGL(dfm_group_scan, dim3(1), dim3(1024), 0, st, count, M, start);
+    hipLaunchKernelGGL(dfm_group_scatter, dim3(nblk), dim3(256), 0, st, idx, B, F, key_field, M,
+                       start, cursor, rows, vout);
+    *rows_out = rows;
+    return vout;
+  }
   uint32_t* kin = reinterpret_cast<uint32_t*>(p);
   uint32_t* kout = reinterpret_cast<uint32_t*>(p + col);
   int32_t* vin = reinterpret_cast<int32_t*>(p + 2 * col);
-  int32_t* vout = reinterpret_cast<int32_t*>(p + 3 * col);
   size_t tmp = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, kin, kout, vin, vout, (int)B, 0,
                                            dfm_key_bits(M), st);

@@ -247,3 +247,41 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
     assert np.all(np.abs(got - ref) <= tol * mag), np.max(np.abs(got - ref) / mag)
     assert np.all(np.abs(got - direct) <= tol * mag), np.max(np.abs(got - direct) / mag)
 
+
+
+@pytest.mark.parametrize("M,users", [(997, 40), (20000, 300)])
+def test_dfm_item_grouping(M, users):
+    """ITEM mode's row grouping (the forward regroups its rows by user: a
+    counting sort for tables up to 16 K rows, hipCUB's radix sort above) puts
+    every score back at its caller's row: equal to the direct kernel within
+    the bf16 tolerance, and to a call on the same rows in another order."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(M)
+    F, k, B = 5, 64, 6000
+    m = _model((users, 400, M, F, k, [150, 200, 150]), mlp_dtype=torch.bfloat16,
+               table_dtype=torch.bfloat16)
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    X[:, 0] = rng.integers(0, users, B)
+    X[:, 2] = M - 7 + X[:, 2] % 7
+    X[:, 3] = M - 9 + X[:, 3] % 2
+    X[:, 4] = M - 12 + X[:, 4] % 3
+    W = m.get_weights()
+    Ls = [W[f"layer_{i}"] for i in range(3)]
+    Bs = [W[f"bias_{i}"] for i in range(3)]
+    E, w = bf16_round(W["feature_embeddings"]), W["feature_bias"][:, 0]
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    Wt, bs, dims, Wpd, bpd = m._prepared()
+    wb = m.weights["feature_bias"].reshape(-1)
+    xd = torch.from_numpy(X).cuda()
+    got = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.bfloat16, Wpd, bpd,
+                          proj="item").cpu().numpy()
+    direct = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.bfloat16, Wpd, bpd,
+                             proj=False).cpu().numpy()
+    perm = rng.permutation(B)
+    again = ops.dfm_forward(xd[torch.from_numpy(perm).cuda()], m.table, wb, Wt, bs, dims,
+                            torch.bfloat16, Wpd, bpd, proj="item").cpu().numpy()
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+    assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
+    assert np.all(np.abs(got - direct) <= 5e-3 * mag)
+    assert np.array_equal(again, got[perm])   # a row's score never depends on its block
