@@ -99,6 +99,24 @@ HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// One lane-linear 16-B-per-lane LDS-DMA (global_load_lds_dwordx4, M0 = the
+// wave's LDS destination) issued through inline asm.  When the compiler sees
+// the DMA builtin it treats it as an LDS access of unknown order and drains
+// every ds_read with lgkmcnt(0) at each MFMA step boundary; issued this way
+// it keeps counted lgkmcnt waits (1 % on C5 ITEM/CTX, profiles/r02_k3_hidden_knockouts.txt).
+// The compiler does not track these loads: every barrier that publishes them
+// is preceded by an explicit s_waitcnt vmcnt(0) (dma_wait below).
+HHFM_DEV void lds_dma16(const void* gsrc, void* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(gsrc), "s"(m0v)
+               : "memory");
+}
+
+HHFM_DEV void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 HHFM_DEV void swap_halves(uint32_t& a, uint32_t& b) {
   // lanes 32-63 of a <-> lanes 0-31 of b
   const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
@@ -202,10 +220,16 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
   auto dma = [&](int g, int b) {
     const uint4* src = a.packed + (int64_t)g * CU + 64 * wv + l;
     uint4* dst = wbuf0 + b * CU + 64 * wv;
+    // (the asm form pays off where the projected kernels' staged P reads sit
+    // between the DMAs and the MFMAs: -1 % there, +1.5 % on the direct kernel)
 #pragma unroll
-    for (int q = 0; q < TM; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(src + 256 * q), (void*)(dst + 256 * q), 16,
-                                       0, 0);
+    for (int q = 0; q < TM; ++q) {
+      if constexpr (PROJ)
+        lds_dma16(src + 256 * q, dst + 256 * q);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(src + 256 * q), (void*)(dst + 256 * q),
+                                         16, 0, 0);
+    }
   };
   // A fragment of tile t, k16 step s of a chunk: row 32t + r, unit 2s + h
   const int swz = (r >> 1) & 7;
@@ -275,11 +299,15 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
 
   auto body = [&](auto stc) {
     constexpr bool ST = decltype(stc)::value;
+    // (the projected kernels' first P field initialises the accumulators)
     f32x16 acc[TM];
+  #ifndef HHFM_KO_PROJP
+    if constexpr (!PROJ)
+  #endif
   #pragma unroll
-    for (int t = 0; t < TM; ++t)
+      for (int t = 0; t < TM; ++t)
   #pragma unroll
-      for (int x = 0; x < 16; ++x) acc[t][x] = 0.f;
+        for (int x = 0; x < 16; ++x) acc[t][x] = 0.f;
     float fs[8], fq[8];
     float y2 = 0.f;
 
@@ -360,7 +388,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         }
       }
     }
-    __syncthreads();   // vmcnt(0): chunk 0, the staged rows and the Σw terms landed
+    dma_wait();
+    __syncthreads();   // chunk 0, the staged rows and the Σw terms landed
     if constexpr (PROJ) {
       float* pst = reinterpret_cast<float*>(smem + kPst);
       const float* P = reinterpret_cast<const float*>(a.proj);
@@ -372,32 +401,43 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
       // (Diagnostic knock-outs, never in the product build: HHFM_KO_PROJP /
       // HHFM_KO_PROJFM skip the P / FM loads — scripts/build_variants.sh.)
   #ifndef HHFM_KO_PROJP
-      for (int f = Fd; f < F; ++f) {
-        // P in accumulator order: positions 32t + 16h .. +15 are this lane's
-        // units of tile t (64 contiguous bytes), from LDS when staged; all
-        // 4·TM reads of a field in flight (a tile-outer order, each tile's
-        // fields summed in registers first, ran 6 % slower)
-        auto addp = [&](const float4* pp) {
+      // P in accumulator order: positions 32t + 16h .. +15 are this lane's
+      // units of tile t (64 contiguous bytes), from LDS when staged; all 4·TM
+      // reads of a field in flight (a tile-outer order, each tile's fields
+      // summed in registers first, ran 6 % slower).  The first field is
+      // written, the others added (an accumulator add is a read-modify-write
+      // of an AGPR).
+      auto addp = [&](const float4* pp, auto first) {
   #pragma unroll
-          for (int t = 0; t < TM; ++t)
+        for (int t = 0; t < TM; ++t)
   #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-              const float4 x = pp[8 * t + g4];
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const float4 x = pp[8 * t + g4];
+            if constexpr (decltype(first)::value) {
+              acc[t][4 * g4 + 0] = x.x;
+              acc[t][4 * g4 + 1] = x.y;
+              acc[t][4 * g4 + 2] = x.z;
+              acc[t][4 * g4 + 3] = x.w;
+            } else {
               acc[t][4 * g4 + 0] += x.x;
               acc[t][4 * g4 + 1] += x.y;
               acc[t][4 * g4 + 2] += x.z;
               acc[t][4 * g4 + 3] += x.w;
             }
-        };
+          }
+      };
+      auto prow = [&](int f) {
         if constexpr (ST)
-          addp(reinterpret_cast<const float4*>(pst + plo[2 * kFusedMaxF + f] +
-                                               (ids[myrow * F + f] - plo[f]) * kPsLd) +
-               4 * h);
+          return reinterpret_cast<const float4*>(pst + plo[2 * kFusedMaxF + f] +
+                                                 (ids[myrow * F + f] - plo[f]) * kPsLd) +
+                 4 * h;
         else
-          addp(reinterpret_cast<const float4*>(P + (f - Fd) * a.proj_fstride +
-                                               (int64_t)ids[myrow * F + f] * a.proj_ld) +
-               4 * h);
-      }
+          return reinterpret_cast<const float4*>(P + (f - Fd) * a.proj_fstride +
+                                                 (int64_t)ids[myrow * F + f] * a.proj_ld) +
+                 4 * h;
+      };
+      addp(prow(Fd), BoolC<true>{});   // Fd < F whenever P is planned
+      for (int f = Fd + 1; f < F; ++f) addp(prow(f), BoolC<false>{});
   #endif
       // FM second-order part (DFM.py:114-122): the lane half h takes columns
       // 16j + 8h .. +7 of every 16-column block j, as the direct kernel's side()
@@ -553,7 +593,8 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
         adv(cs);
       };
       run_chunk(b, bop, side);
-      __syncthreads();   // vmcnt(0): chunk c+1's weights and embeddings landed
+      dma_wait();
+      __syncthreads();   // chunk c+1's weights and embeddings landed
     };
     // (two register sets alternate, so no copy of the gathered chunk is needed
     // on the loop's back edge)
@@ -602,6 +643,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
           return __builtin_bit_cast(bf16x8, bx);
         };
         run_chunk(b, bop, [](int) {});
+        dma_wait();
         __syncthreads();
       }
     }
