@@ -1206,28 +1206,29 @@ __global__ __launch_bounds__(256) void dfm_gather_rows(const int32_t* __restrict
 }
 
 // Counting-sort grouping for key ranges up to kGroupBins ids (Frappe's users:
-// 957 of 5,051 table rows): every block histograms its slice of rows in LDS,
+// 957 of 5,051 table rows): every 1024-thread block (16 waves: the loops are
+// dependent-load chains, occupancy hides them) histograms its slice in LDS,
 // reserves one range per (block, id) with a global atomic, and scatters its
 // rows straight into the grouped copy (and their positions into the order).
 // Positions inside one id's group depend on atomic timing — every row's
 // arithmetic does not, so the scores are identical either way.  Larger key
 // ranges take hipCUB's radix sort.
-constexpr int kGroupBins = 16384;
+constexpr int kGroupBins = 8192;
 constexpr int kGroupRows = 8192;   // rows per block
 
-__global__ __launch_bounds__(256) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
+__global__ __launch_bounds__(1024) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
                                                       int F, int key_field, int64_t M,
                                                       uint32_t* __restrict__ count) {
   __shared__ uint32_t hcnt[kGroupBins];
   const int nb = (int)M;
-  for (int b = threadIdx.x; b < nb; b += 256) hcnt[b] = 0;
+  for (int b = threadIdx.x; b < nb; b += 1024) hcnt[b] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
   const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256)
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024)
     atomicAdd(&hcnt[clamp_id(idx[m * F + key_field], M)], 1u);
   __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += 256)
+  for (int b = threadIdx.x; b < nb; b += 1024)
     if (hcnt[b]) atomicAdd(&count[b], hcnt[b]);
 }
 
@@ -1254,26 +1255,26 @@ __global__ __launch_bounds__(1024) void dfm_group_scan(const uint32_t* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void dfm_group_scatter(const int32_t* __restrict__ idx,
-                                                         int64_t B, int F, int key_field,
-                                                         int64_t M,
-                                                         const uint32_t* __restrict__ start,
-                                                         uint32_t* __restrict__ cursor,
-                                                         int32_t* __restrict__ rows,
-                                                         int32_t* __restrict__ order) {
+__global__ __launch_bounds__(1024) void dfm_group_scatter(const int32_t* __restrict__ idx,
+                                                          int64_t B, int F, int key_field,
+                                                          int64_t M,
+                                                          const uint32_t* __restrict__ start,
+                                                          uint32_t* __restrict__ cursor,
+                                                          int32_t* __restrict__ rows,
+                                                          int32_t* __restrict__ order) {
   __shared__ uint32_t hpos[kGroupBins];
   const int nb = (int)M;
-  for (int b = threadIdx.x; b < nb; b += 256) hpos[b] = 0;
+  for (int b = threadIdx.x; b < nb; b += 1024) hpos[b] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
   const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256)
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024)
     atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
   __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += 256)   // this block's range inside id b's group
+  for (int b = threadIdx.x; b < nb; b += 1024)   // this slice's range inside id b's group
     if (hpos[b]) hpos[b] = start[b] + atomicAdd(&cursor[b], hpos[b]);
   __syncthreads();
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 256) {
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024) {
     const uint32_t pos = atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
     for (int f = 0; f < F; ++f) rows[(int64_t)pos * F + f] = idx[m * F + f];
     order[pos] = (int32_t)m;
@@ -1308,11 +1309,11 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
     uint32_t* start = reinterpret_cast<uint32_t*>(tmp_ws + 2 * mb);
     if (hipMemsetAsync(count, 0, 2 * mb, st) != hipSuccess) return nullptr;
     const unsigned nblk = (unsigned)((B + kGroupRows - 1) / kGroupRows);
-    hipLaunchKernelGGL(dfm_group_hist, dim3(nblk), dim3(256), 0, st, idx, B, F, key_field, M,
+    hipLaunchKernelGGL(dfm_group_hist, dim3(nblk), dim3(1024), 0, st, idx, B, F, key_field, M,
                        count);
     hipLaunchKernelGGL(dfm_group_scan, dim3(1), dim3(1024), 0, st, count, M, start);
-    hipLaunchKernelGGL(dfm_group_scatter, dim3(nblk), dim3(256), 0, st, idx, B, F, key_field, M,
-                       start, cursor, rows, vout);
+    hipLaunchKernelGGL(dfm_group_scatter, dim3(nblk), dim3(1024), 0, st, idx, B, F, key_field,
+                       M, start, cursor, rows, vout);
     *rows_out = rows;
     return vout;
   }

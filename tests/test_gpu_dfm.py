@@ -252,7 +252,7 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
 @pytest.mark.parametrize("M,users", [(997, 40), (20000, 300)])
 def test_dfm_item_grouping(M, users):
     """ITEM mode's row grouping (the forward regroups its rows by user: a
-    counting sort for tables up to 16 K rows, hipCUB's radix sort above) puts
+    counting sort for tables up to 8 K rows, hipCUB's radix sort above) puts
     every score back at its caller's row: equal to the direct kernel within
     the bf16 tolerance, and to a call on the same rows in another order."""
     from hhfm_amd import ops
