@@ -318,16 +318,22 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
     // accesses complete in order, so no barrier.)
     float4* ep = reinterpret_cast<float4*>(apl + NA) + 32 * wv;
     if (h == 0) ep[j] = make_float4(lg, sP, wf, 0.f);
-    if (ok && p == 0 && h == 0) {
+    // every combo's lane takes its own exp (the row's max read back from the
+    // parked logits) — one lane per row taking all np exps in turn was 15 % of
+    // the kernel — then the row's first lane sums in the reference's order
+    if (h == 0 && live) {
       const float4* e = ep + r * np;
       float mx = kNegInf;
       for (int q = 0; q < np; ++q) mx = fmaxf(mx, e[q].x);
+      ep[j].w = expf(lg - mx);
+    }
+    if (ok && p == 0 && h == 0) {
+      const float4* e = ep + r * np;
       float se = 0.f, num = 0.f;
       for (int q = 0; q < np; ++q) {
         const float4 eq = e[q];
-        const float ee = expf(eq.x - mx);
-        se += ee;
-        num = fmaf(ee, eq.y, num);
+        se += eq.w;
+        num = fmaf(eq.w, eq.y, num);
       }
       float fb = 0.f;
       if (np >= F) {   // the row's lanes fetched one field each
