@@ -285,3 +285,34 @@ def test_dfm_item_grouping(M, users):
     assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
     assert np.all(np.abs(got - direct) <= 5e-3 * mag)
     assert np.array_equal(again, got[perm])   # a row's score never depends on its block
+
+
+def test_dfm_catalog_item_column_permuted():
+    """ITEM mode keeps the catalog's item column on MFMA whichever column it
+    is (here 2: the kernel's field order becomes [2, 0, 1, 3, 4] and layer
+    0's packed weights, the projection and the Σw weights follow it), against
+    the bf16-rounding oracle's top-K."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(21)
+    nu, ni, F, k = 50, 600, 5, 32
+    M = nu + ni + 12
+    m = _model((nu, ni, M, F, k, [64, 48]), mlp_dtype=torch.bfloat16)
+    A = np.stack([rng.integers(0, nu, 29), rng.integers(nu + ni, nu + ni + 7, 29),
+                  rng.integers(nu, nu + ni, 29), rng.integers(nu + ni + 7, nu + ni + 9, 29),
+                  rng.integers(nu + ni + 9, M, 29)], 1).astype(np.int32)
+    W = m.get_weights()
+    Ls = [W["layer_0"], W["layer_1"]]
+    Bs = [W["bias_0"], W["bias_1"]]
+    rows = np.repeat(A, ni, 0)
+    rows[:, 2] = np.tile(np.arange(nu, nu + ni), len(A))
+    sc = _bf16_oracle(rows, W["feature_embeddings"], W["feature_bias"][:, 0], Ls, Bs,
+                      W["concat_projection"], float(W["concat_bias"])).reshape(len(A), ni)
+    Wt, bs, dims, Wp, bp = m._prepared()
+    q = torch.from_numpy(A).cuda()
+    rs, ri = orc.top_k(sc, 20)
+    tol = 5e-3 * np.abs(sc).max(1, keepdims=True)
+    for proj in (False, "item"):
+        s, i = ops.dfm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, bs,
+                                    dims, Wp, bp, 2, nu, ni, 20, 0, 1 << 20, proj=proj)
+        bad, swaps = orc.topk_swaps(sc, ri, i.cpu().numpy(), tol)
+        assert bad == 0 and swaps == 0, (proj, bad, swaps)
