@@ -1206,15 +1206,20 @@ __global__ __launch_bounds__(256) void dfm_gather_rows(const int32_t* __restrict
 }
 
 // Counting-sort grouping for key ranges up to kGroupBins ids (Frappe's users:
-// 957 of 5,051 table rows): every 1024-thread block (16 waves: the loops are
-// dependent-load chains, occupancy hides them) histograms its slice in LDS,
-// reserves one range per (block, id) with a global atomic, and scatters its
-// rows straight into the grouped copy (and their positions into the order).
-// Positions inside one id's group depend on atomic timing — every row's
-// arithmetic does not, so the scores are identical either way.  Larger key
-// ranges take hipCUB's radix sort.
+// 957 of 5,051 table rows).  dfm_group_hist: every 1024-thread block
+// histograms an 8 K-row slice in LDS and adds it to the global counts;
+// dfm_group_scan turns them into group starts.  dfm_group_scatter then sorts
+// its 4 K-row slice by key in LDS (a local counting sort: per-row rank from
+// the LDS atomic, a block scan, one global reservation per (slice, id)) and
+// writes the grouped copy dword by dword in sorted order, so consecutive
+// lanes store consecutive words of one id's run (a per-row scatter of 4-B
+// words to random runs cost 3.4x as much at 12.5 M rows:
+// scripts/diag/groupbench.hip).  Positions inside one id's group depend on
+// atomic timing — every row's arithmetic does not, so the scores are
+// identical either way.  Larger key ranges take hipCUB's radix sort.
 constexpr int kGroupBins = 8192;
-constexpr int kGroupRows = 8192;   // rows per block
+constexpr int kGroupRows = 8192;      // rows per histogram block
+constexpr int kScatterRows = 4096;    // rows per scatter block (<= 65536: 16-bit local index)
 
 __global__ __launch_bounds__(1024) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
                                                       int F, int key_field, int64_t M,
@@ -1262,22 +1267,63 @@ __global__ __launch_bounds__(1024) void dfm_group_scatter(const int32_t* __restr
                                                           uint32_t* __restrict__ cursor,
                                                           int32_t* __restrict__ rows,
                                                           int32_t* __restrict__ order) {
-  __shared__ uint32_t hpos[kGroupBins];
+  constexpr int kPer = kScatterRows / 1024;
+  __shared__ uint32_t lstart[kGroupBins];   // slice count, then local group start
+  __shared__ int32_t delta[kGroupBins];     // global group position - local start
+  __shared__ uint32_t lrow[kScatterRows];   // sorted slot -> key << 16 | local row
+  __shared__ uint32_t wsum[16];
   const int nb = (int)M;
-  for (int b = threadIdx.x; b < nb; b += 1024) hpos[b] = 0;
+  for (int b = threadIdx.x; b < nb; b += 1024) lstart[b] = 0;
   __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
-  const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024)
-    atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
+  const int64_t r0 = (int64_t)blockIdx.x * kScatterRows;
+  const int n = (int)(r0 + kScatterRows < B ? kScatterRows : B - r0);
+  int key[kPer];
+  uint32_t rank[kPer];
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int j = threadIdx.x + i * 1024;
+    if (j < n) {
+      key[i] = clamp_id(idx[(r0 + j) * F + key_field], M);
+      rank[i] = atomicAdd(&lstart[key[i]], 1u);
+    }
+  }
   __syncthreads();
-  for (int b = threadIdx.x; b < nb; b += 1024)   // this slice's range inside id b's group
-    if (hpos[b]) hpos[b] = start[b] + atomicAdd(&cursor[b], hpos[b]);
+  // exclusive block scan of the slice counts: a chunk of bins per thread,
+  // wave-level inclusive scan of the chunk sums, then the waves' totals
+  const int per = (nb + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  uint32_t s = 0;
+  for (int b = b0; b < b0 + per && b < nb; ++b) s += lstart[b];
+  uint32_t inc = s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t v = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += v;
+  }
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024) {
-    const uint32_t pos = atomicAdd(&hpos[clamp_id(idx[m * F + key_field], M)], 1u);
-    for (int f = 0; f < F; ++f) rows[(int64_t)pos * F + f] = idx[m * F + f];
-    order[pos] = (int32_t)m;
+  uint32_t run = inc - s;
+  for (int i = 0; i < w; ++i) run += wsum[i];
+  for (int b = b0; b < b0 + per && b < nb; ++b) {
+    const uint32_t c = lstart[b];
+    lstart[b] = run;
+    delta[b] = c ? (int32_t)(start[b] + atomicAdd(&cursor[b], c)) - (int32_t)run : 0;
+    run += c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int j = threadIdx.x + i * 1024;
+    if (j < n) lrow[lstart[key[i]] + rank[i]] = ((uint32_t)key[i] << 16) | (uint32_t)j;
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < n * F; x += 1024) {   // word f of sorted slot j
+    const int j = x / F, f = x - j * F;
+    const uint32_t e = lrow[j];
+    const int jl = (int)(e & 0xffff);
+    const int64_t pos = (int64_t)delta[e >> 16] + j;
+    rows[pos * F + f] = idx[(r0 + jl) * F + f];
+    if (f == 0) order[pos] = (int32_t)(r0 + jl);
   }
 }
 
@@ -1312,7 +1358,8 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
     hipLaunchKernelGGL(dfm_group_hist, dim3(nblk), dim3(1024), 0, st, idx, B, F, key_field, M,
                        count);
     hipLaunchKernelGGL(dfm_group_scan, dim3(1), dim3(1024), 0, st, count, M, start);
-    hipLaunchKernelGGL(dfm_group_scatter, dim3(nblk), dim3(1024), 0, st, idx, B, F, key_field,
+    const unsigned sblk = (unsigned)((B + kScatterRows - 1) / kScatterRows);
+    hipLaunchKernelGGL(dfm_group_scatter, dim3(sblk), dim3(1024), 0, st, idx, B, F, key_field,
                        M, start, cursor, rows, vout);
     *rows_out = rows;
     return vout;

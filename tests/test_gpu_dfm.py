@@ -249,7 +249,7 @@ def test_dfm_projected_layer0(F, k, layers, tdt, B, mlp, proj):
 
 
 
-@pytest.mark.parametrize("M,users", [(997, 40), (20000, 300)])
+@pytest.mark.parametrize("M,users", [(997, 40), (8100, 6000), (20000, 300)])
 def test_dfm_item_grouping(M, users):
     """ITEM mode's row grouping (the forward regroups its rows by user: a
     counting sort for tables up to 8 K rows, hipCUB's radix sort above) puts
