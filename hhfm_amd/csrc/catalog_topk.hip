@@ -41,8 +41,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
 #endif
+#ifndef HHFM_RING_PAIR
+#define HHFM_RING_PAIR 0   // 1: catalog_ring bf16 with one s_barrier per two tiles (6-slot ring; measured neutral at C4, 1.20 vs 1.21 ms)
+#endif
 #ifndef HHFM_RING_SLOTS
-#define HHFM_RING_SLOTS 4   // catalog_ring bf16 tile slots (R-1 tiles of DMA lead)
+// catalog_ring bf16 tile slots: R-1 tiles of DMA lead, or (pairs) R-2
+#define HHFM_RING_SLOTS (HHFM_RING_PAIR ? 6 : 4)
 #endif
 #ifndef HHFM_MAIN_PF
 #define HHFM_MAIN_PF 1   // item tiles in flight per wave (1 or 2)
@@ -511,6 +515,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   constexpr int64_t ROWB = Cfg::kRowB;
   constexpr int NU = Cfg::kNU;
   constexpr int R = Cfg::kSlots;
+  constexpr bool kPair = BF16 && HHFM_RING_PAIR;   // tiles 2i, 2i+1 behind one barrier
   static_assert(BF16 ? KT % kRingWaves == 0 : true, "ring kernel: bf16 k >= 16 * waves");
 
   __shared__ __attribute__((aligned(16))) char smem[Cfg::kSmem];
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   float wnext = 0.f;
   if (tb0 < tb1) {
     if constexpr (BF16) {
-      for (int s = 0; s < R - 1; ++s) dma_tile(tb0 + s, s);
+      for (int s = 0; s < (kPair ? R - 2 : R - 1); ++s) dma_tile(tb0 + s, s);
     } else {
       load_unit(tb0, rawA);
       load_unit(tb0 + 1, rawB);
@@ -661,21 +666,33 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   };
 
   // one tile: raw sets (cur holds tile+1's unit, nxt receives tile+3's) for fp32
-  auto tile_step = [&](const int tile, uint4 (&cur)[NUL][2], uint4 (&nxt)[NUL][2]) {
+  // sync: publish the stage (every fp32 tile; bf16 pairs: the first tile of
+  // each pair, whose barrier also covers the second)
+  auto tile_step = [&](const int tile, uint4 (&cur)[NUL][2], uint4 (&nxt)[NUL][2],
+                       const bool sync) {
     const int it = tile - tb0;
     // ---- publish: tile's stage complete and the previous tile's stage free ----
-    if constexpr (BF16) {
-      // DMA of `tile` is older than the (R-2) tiles issued after it
-      HHFM_VMCNT((R - 2) * Cfg::kDma);
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's piece stores landed
-    __builtin_amdgcn_s_barrier();
-    if constexpr (BF16) {
-      if (tile + R - 1 < tb1) dma_tile(tile + R - 1, (it + R - 1) % R);
-    } else {
-      // split tile+1 into the other piece buffer, then fetch tile+3's unit
-      if (tile + 1 < tb1) store_pieces(cur, (it + 1) & 1);
-      if (tile + 3 < tb1) load_unit(tile + 3, cur);
+    if (sync) {
+      // bf16: every step issues its DMAs unconditionally (tiles past the split
+      // re-read its last tile into a free slot), so the count of tiles issued
+      // after this one is exact up to the split's end: R-2, or (pairs) the
+      // next pair's 2
+      if constexpr (kPair)
+        HHFM_VMCNT(2 * Cfg::kDma);
+      else if constexpr (BF16)
+        HHFM_VMCNT((R - 2) * Cfg::kDma);
+      __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's piece stores landed
+      __builtin_amdgcn_s_barrier();
+      if constexpr (kPair) {   // into the previous pair's slots
+        dma_tile(tile + 4, (it + 4) % R);
+        dma_tile(tile + 5, (it + 5) % R);
+      } else if constexpr (BF16) {
+        dma_tile(tile + R - 1, (it + R - 1) % R);
+      } else {
+        // split tile+1 into the other piece buffer, then fetch tile+3's unit
+        if (tile + 1 < tb1) store_pieces(cur, (it + 1) & 1);
+        if (tile + 3 < tb1) load_unit(tile + 3, cur);
+      }
     }
     (void)nxt;
     float wcur = wnext;
@@ -752,8 +769,8 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
     }
   };
   for (int tile = tb0; tile < tb1; tile += 2) {
-    tile_step(tile, rawB, rawA);
-    if (tile + 1 < tb1) tile_step(tile + 1, rawA, rawB);
+    tile_step(tile, rawB, rawA, true);
+    if (tile + 1 < tb1) tile_step(tile + 1, rawA, rawB, !kPair);
   }
 #undef HHFM_VMCNT
   if (!wave_live) return;
