@@ -1,7 +1,10 @@
 // Diagnostic (not product): the DeepFM ITEM-projection row grouping
 // (dfm_fused.hip dfm_order_rows, counting-sort branch) at the C5 bench shape
 // (12.5 M rows, F = 5, 957 users, key field 0), current scatter against a
-// slice-local sort whose writes are ordered (dword-parallel runs per user).
+// slice-local sort whose writes are ordered (dword-parallel runs per user;
+// "ord" — the product's dfm_group_scatter, which additionally limits its bins
+// to the slice's key range) and per-row ordered writes ("ordrow").  Bins here
+// = the 957 users; results in profiles/r02_groupbench.txt.
 // Prints ms per grouping (best of 7) and checks each variant's output.
 #include <hip/hip_runtime.h>
 #include <cstdio>
