@@ -923,11 +923,24 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   for (int64_t b = wave; b < B; b += nwave) {
     float as = kNegInf;
     int32_t ai = kNoIdx;
-    for (int r = 0; r < R; ++r) {
-      const int64_t off = r * stride_r + b * stride_b;
-      float bs = l < K ? in_s[off + l] : kNegInf;
-      int32_t bi = l < K ? in_i[off + l] : kNoIdx;
-      merge_lists<KPAD>(as, ai, bs, bi);
+    // lists in groups of kPF: a group's loads are all in flight before its
+    // merges (one load latency per group instead of per list); lists past R
+    // are empty (-inf, no index) and merge as no-ops, so the result is the
+    // sequential merge's
+    constexpr int kPF = 8;
+    for (int r0 = 0; r0 < R; r0 += kPF) {
+      float bs[kPF];
+      int32_t bi[kPF];
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) {
+        const int r = r0 + u;
+        const bool ok = r < R && l < K;
+        const int64_t off = (int64_t)(r < R ? r : 0) * stride_r + b * stride_b;
+        bs[u] = ok ? in_s[off + l] : kNegInf;
+        bi[u] = ok ? in_i[off + l] : kNoIdx;
+      }
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) merge_lists<KPAD>(as, ai, bs[u], bi[u]);
     }
     if (l < K) {
       out_s[b * K + l] = as;
