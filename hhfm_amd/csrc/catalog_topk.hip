@@ -924,23 +924,51 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
     float as = kNegInf;
     int32_t ai = kNoIdx;
     // lists in groups of kPF: a group's loads are all in flight before its
-    // merges (one load latency per group instead of per list); lists past R
-    // are empty (-inf, no index) and merge as no-ops, so the result is the
-    // sequential merge's
+    // merges (one load latency per group instead of per list).  KPAD = 32:
+    // the two 32-lane halves merge the even and the odd lists side by side,
+    // then the odd half's list is merged into the even half's.  Every merge
+    // keeps the top KPAD of a union under the strict (score desc, id asc)
+    // order, so the result is the sequential merge's; lists past R are empty
+    // (-inf, no index) and merge as no-ops.
     constexpr int kPF = 8;
-    for (int r0 = 0; r0 < R; r0 += kPF) {
+    constexpr int kHalves = KPAD == 32 ? 2 : 1;
+    const int h = kHalves == 2 ? l >> 5 : 0;
+    const int lh = l & (KPAD - 1);
+    for (int r0 = 0; r0 < R; r0 += kPF * kHalves) {
       float bs[kPF];
       int32_t bi[kPF];
 #pragma unroll
       for (int u = 0; u < kPF; ++u) {
-        const int r = r0 + u;
-        const bool ok = r < R && l < K;
+        const int r = r0 + u * kHalves + h;
+        const bool ok = r < R && lh < K;
         const int64_t off = (int64_t)(r < R ? r : 0) * stride_r + b * stride_b;
-        bs[u] = ok ? in_s[off + l] : kNegInf;
-        bi[u] = ok ? in_i[off + l] : kNoIdx;
+        bs[u] = ok ? in_s[off + lh] : kNegInf;
+        bi[u] = ok ? in_i[off + lh] : kNoIdx;
       }
 #pragma unroll
-      for (int u = 0; u < kPF; ++u) merge_lists<KPAD>(as, ai, bs[u], bi[u]);
+      for (int u = 0; u < kPF; ++u) {
+        if constexpr (kHalves == 2) {
+          const int src = (h << 5) + (31 - lh);   // reverse within the half
+          const float rs = shfl_f(bs[u], src);
+          const int32_t ri = shfl_i(bi[u], src);
+          if (better(rs, ri, as, ai)) {
+            as = rs;
+            ai = ri;
+          }
+          bitonic_merge_desc<32>(as, ai);
+        } else {
+          merge_lists<KPAD>(as, ai, bs[u], bi[u]);
+        }
+      }
+    }
+    if constexpr (kHalves == 2) {   // the odd half's list into the even half's
+      const float rs = shfl_f(as, 32 + (31 - lh));
+      const int32_t ri = shfl_i(ai, 32 + (31 - lh));
+      if (h == 0 && better(rs, ri, as, ai)) {
+        as = rs;
+        ai = ri;
+      }
+      bitonic_merge_desc<32>(as, ai);
     }
     if (l < K) {
       out_s[b * K + l] = as;
