@@ -41,6 +41,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
 #endif
+#ifndef HHFM_SEED_MAX
+#define HHFM_SEED_MAX 32768   // items of the threshold seed, at most
+#endif
 #ifndef HHFM_RING_PAIR
 #define HHFM_RING_PAIR 0   // 1: catalog_ring bf16 with one s_barrier per two tiles (6-slot ring; measured neutral at C4, 1.20 vs 1.21 ms)
 #endif
@@ -1079,7 +1082,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   p.seed_n = 0;
   if (!p.small && !p.dense && catalog_seed()) {
     int64_t sn = ((int64_t)32 << 20) / p.Bpad;
-    sn = (sn > 32768 ? 32768 : sn) & ~int64_t(31);
+    sn = (sn > HHFM_SEED_MAX ? HHFM_SEED_MAX : sn) & ~int64_t(31);
     if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
   }
   p.off_seed_sc = off;
