@@ -61,6 +61,8 @@ def parse():
                         "12.5M rows per GPU)")
     p.add_argument("--hr-epochs", type=int, default=5)
     p.add_argument("--c5-rows", type=int, default=12_500_000)
+    p.add_argument("--no-check", action="store_true",
+                   help="skip the legs' oracle parity checks (timing only)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: every rank joins a gloo group and "
                         "rank 0 prints the world it saw")
@@ -152,6 +154,7 @@ def cpu_baseline(idx, E, w, w0, out_gpu, args):
     box's CPU share), and every core of the affinity mask.  Also the GPU's
     parity on a subset, elementwise and normwise."""
     from oracle import cpu as ocpu
+    from oracle import parity
     aff = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
     n = min(args.cpu_rows, idx.shape[0])
@@ -182,10 +185,12 @@ def cpu_baseline(idx, E, w, w0, out_gpu, args):
     m = min(n, 1 << 16)                                 # parity spot-check subset
     got = out_gpu[:m].cpu().numpy().astype(np.float64)
     rf = ref[:m].astype(np.float64)
-    e = Eh[X[:m].astype(np.int64)].astype(np.float64)
-    scale = (0.5 * (e.sum(1) ** 2 + (e * e).sum(1))).sum(1) + np.abs(wh[X[:m]]).sum(1) + abs(w0)
+    ex, scale = parity.fm_rows_exact(X[:m], Eh, wh, w0)
     err = np.abs(got - rf)
     rel = err / np.maximum(np.abs(rf), 1e-30)
+    vs_exact = parity.row_check(got, ex, scale)
+    vs_exact["cpu_oracle_max_rel_err_kappa_le_max"] = parity.row_check(
+        rf, ex, scale)["max_rel_err_kappa_le_max"]
     return {"value": best["triples_per_s"], "unit": "triples/s", "cores": best["threads"],
             "kind": "port",
             "sample": f"first {n} rows of the same batch (same 4.3 GB table), "
@@ -198,7 +203,11 @@ def cpu_baseline(idx, E, w, w0, out_gpu, args):
                            "max_rel_err_normwise": float((err / scale).max()),
                            "note": "elementwise |gpu-cpu|/|cpu|; rows above 1e-5 are "
                                    "cancellations ((Σv)²≈Σv², |out| << Σ|terms|), bounded "
-                                   "by the normwise figure"}}
+                                   "by the normwise figure"},
+            "gpu_vs_float64": dict(vs_exact, note=(
+                "GPU rows vs the float64 value of FM.py:99-120 (oracle/parity.row_check): "
+                "rows with κ = Σ|terms|/|out| <= 100 within 1e-5 relative, the rest within "
+                "1e-5 of Σ|terms|; the fp32 C oracle's own error on the same rows beside it"))}
 
 
 def frappe_shape_dataset(path, rows=96203, seed=11):
@@ -268,11 +277,45 @@ def hr_leg(dev, epochs):
             "epoch_loss": losses, "train_s": t_train}
 
 
+def _oracle_threads():
+    aff = len(os.sched_getaffinity(0))
+    return min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff, aff)
+
+
+def _topk_parity(got_s, got_i, ref_i, exact, rel=1e-5):
+    """Top-K parity record (oracle/parity.py contract): ids equal to the
+    oracle's at every position but float64-verified fp32 ties (counted), every
+    returned score within 1e-5 relative of its float64 value, lists sorted."""
+    from oracle import parity
+    got_s = np.asarray(got_s)
+    got_i = np.asarray(got_i)
+    bad, swaps, dup = parity.topk_tie_count(got_i, ref_i, exact)
+    ex = np.empty(got_s.shape)
+    mag = np.empty(got_s.shape)
+    for b in range(got_i.shape[0]):
+        ex[b], mag[b] = exact(b, got_i[b])
+    err = np.abs(got_s - ex)
+    relerr = float((err / np.maximum(np.abs(ex), 1e-300)).max())
+    normwise = float((err / np.maximum(mag, 1e-300)).max())
+    ordered = bool(np.all(np.diff(got_s, axis=1) <= 0))
+    return {"queries": int(got_i.shape[0]), "positions": int(got_i.size),
+            "ids_equal_to_oracle": bool(np.array_equal(got_i, ref_i)),
+            "tie_swaps": swaps, "unexplained": bad, "duplicates": dup,
+            "max_rel_err_scores_vs_float64": relerr, "max_normwise_err": normwise,
+            "sorted": ordered,
+            "parity": bad == 0 and dup == 0 and ordered and normwise <= rel and relerr <= rel}
+
+
 def catalog_c3_leg(dev, reps=50):
     """configs[2] / C3: HHFM k=64, bf16 table, Frappe vocabulary (957 users,
     4,082 items, ctx 7/2/3), 3,000 queries, top-20 over the full catalog
-    (hhfm_catalog_topk: score matrix by MFMA GEMM + dense top-K)."""
+    (hhfm_catalog_topk: STORE score matrix + dense top-K); beside it the
+    reference's own call shape, one topk(A[300], 20) (FM.py:333-334,
+    OurModel7.py:471), and the 3,000-query top-20 checked against
+    oracle/cpu_oracle.c (same bf16-rounded table)."""
     from hhfm_amd import ops
+    from oracle import cpu as ocpu
+    from oracle import parity
     nu, ni, ctx, k, B = 957, 4082, (7, 2, 3), 64, 3000
     g = torch.Generator(device=dev)
     g.manual_seed(2)
@@ -286,21 +329,41 @@ def catalog_c3_leg(dev, reps=50):
         off += c
     A = torch.stack(cols, 1).to(torch.int32).contiguous()
 
-    def step():
-        return ops.catalog_topk(A, E, ops.MODE_HHFM, 20, nu, ni, 0, None, 0, (2, 5), (0, 0))
+    def timed(Aq, n):
+        def step():
+            return ops.catalog_topk(Aq, E, ops.MODE_HHFM, 20, nu, ni, 0, None, 0, (2, 5),
+                                    (0, 0))
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            step()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / n * 1e3
 
-    for _ in range(5):
-        step()
+    ms = timed(A, reps)
+    A300 = A[:300].contiguous()
+    ms300 = timed(A300, 4 * reps)
+    s, i = ops.catalog_topk(A, E, ops.MODE_HHFM, 20, nu, ni, 0, None, 0, (2, 5), (0, 0))
     torch.cuda.synchronize()
+    Ah = A.cpu().numpy()
+    Ef = E.float().cpu().numpy()
     t0 = time.perf_counter()
-    for _ in range(reps):
-        step()
-    torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) / reps * 1e3
+    rs, ri = ocpu.catalog_topk(Ah, Ef, 1, 20, nu, ni, ctx=(2, 5), threads=_oracle_threads())
+    par = _topk_parity(s.cpu().numpy(), i.cpu().numpy(), ri, parity.hhfm_exact(Ah, Ef, nu))
+    par["oracle"] = "oracle/cpu_oracle.c oracle_catalog_topk mode 1 (OurModel7.py:294 + " \
+                    "tf.nn.top_k order), all 3,000 queries"
+    par["oracle_s"] = time.perf_counter() - t0
     pairs = B * ni
     return {"workload": "C3 (configs[2]): HHFM k=64 bf16 table, Frappe vocabulary, 3,000 "
                         "queries x 4,082 items, top-20, one GPU", "ms_per_query_batch": ms,
-            "pairs_per_s": pairs / (ms * 1e-3), "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12}
+            "pairs_per_s": pairs / (ms * 1e-3), "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12,
+            "reference_call_300_queries_us": ms300 * 1e3,
+            "reference_call_note": "one topk(A[300], 20) as FM.py:333-334 / OurModel7.py:471 "
+                                   "call it (evaluate_TopK's 300-row batches), host-timed "
+                                   "back to back",
+            "parity": par}
 
 
 ITEM_BLOCK = 1 << 16
@@ -327,13 +390,23 @@ def _sha(t):
     return hashlib.sha256(t.contiguous().cpu().numpy().tobytes()).hexdigest()[:16]
 
 
-def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
+# top-20 checksums of the C4 legs at N=1 (profiles/r02_bench_full.json, driver
+# BENCH_r02.json): the catalog is a function of the global item index, so
+# every N must reproduce them (the RCCL all-gather + merge path's check)
+C4_N1_SHA = {"fp32": {"ids": "62574e2b64a438f1", "scores": "6cbbc10b494ce2cc"},
+             "bf16": {"ids": "c7c4f5f1a9d97ea3", "scores": "502206c7ac910a91"}}
+C4_CHECK_QUERIES = 64
+
+
+def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32, check=True):
     """C4: HHFM k=128, 1 M users, 10 M items sharded contiguously over the
     ranks, 1,024 queries, K=20, fp32 (or bf16) table; local
     hhfm_catalog_topk + one packed RCCL all-gather + hhfm_topk_merge per step.
     Table per rank: [users | 12 ctx | this rank's items]; the catalog is a
     function of the global item index (item_rows), so the top-20 checksum is
-    the same for every N."""
+    the same for every N and is compared with the committed N=1 value.
+    Parity (rank 0, every N): the merged top-20 of the first 64 queries
+    against oracle/cpu_oracle.c over the FULL 10 M-item catalog."""
     from hhfm_amd import distributed as hd
     from hhfm_amd import ops
     nu, ni, k, B, K = 1 << 20, 10_000_000, 128, 1024, 20
@@ -344,7 +417,6 @@ def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
     rows_ctx = torch.empty(12, k, device=dev).normal_(0, 0.01, generator=g)
     E = torch.cat([rows_user, rows_ctx, item_rows(begin, end, k, dev)]).to(table_dtype)
     E = E.contiguous()
-    del rows_user
     cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
             torch.zeros(B, dtype=torch.int64, device=dev)]
     off = nu
@@ -352,6 +424,10 @@ def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
         cols.append(torch.randint(0, c, (B,), generator=g, device=dev) + off)
         off += c
     A = torch.stack(cols, 1).to(torch.int32).contiguous()
+    qc = C4_CHECK_QUERIES
+    # the checked queries' user rows + the context rows, as the table stores them
+    check_rows = torch.cat([rows_user[A[:qc, 0].long()], rows_ctx]).to(table_dtype).float()
+    del rows_user
     row0 = nu + 12                       # this rank's first item row
 
     def scorer(A_, b0, cnt, Kl):
@@ -377,16 +453,59 @@ def catalog_leg(dev, world, rank, reps=5, table_dtype=torch.float32):
     ms = float(el[0]) / reps * 1e3
     pairs = B * ni
     tname = "fp32" if table_dtype == torch.float32 else "bf16"
-    return {"workload": f"C4: HHFM k=128 {tname} table, 10M-item catalog sharded over ranks, "
-                        "1,024 queries, top-20 (local split-bf16 MFMA score + select, one "
-                        "packed RCCL all-gather, merge)",
-            "ms_per_query_batch": ms, "pairs_per_s": pairs / (ms * 1e-3),
-            "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world,
-            "top20_ids_sha256": _sha(i), "top20_scores_sha256": _sha(s),
-            "checksum_note": "catalog seeded by global item index: identical for every N"}
+    sha = {"ids": _sha(i), "scores": _sha(s)}
+    res = {"workload": f"C4: HHFM k=128 {tname} table, 10M-item catalog sharded over ranks, "
+                       "1,024 queries, top-20 (local split-bf16 MFMA score + select, one "
+                       "packed RCCL all-gather, merge)",
+           "ms_per_query_batch": ms, "pairs_per_s": pairs / (ms * 1e-3),
+           "TFLOPs": 2.0 * k * pairs / (ms * 1e-3) / 1e12, "ranks": world,
+           "top20_ids_sha256": sha["ids"], "top20_scores_sha256": sha["scores"],
+           "n1_sha256": C4_N1_SHA[tname],
+           "matches_n1": sha == C4_N1_SHA[tname],
+           "checksum_note": "catalog seeded by global item index: every N must reproduce the "
+                            "committed N=1 checksums (bench.py C4_N1_SHA)"}
+    if check and rank == 0:
+        res["parity"] = _c4_parity(E, check_rows, A[:qc], s[:qc], i[:qc], world, row0, ni, k,
+                                   table_dtype, dev)
+    del E
+    return res
 
 
-def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
+def _c4_parity(E, check_rows, Aq, s, i, world, row0, ni, k, table_dtype, dev):
+    """The merged top-20 of the first queries vs oracle/cpu_oracle.c over the
+    whole catalog (OurModel7.py:294 as a k-ordered fp32 chain + tf.nn.top_k
+    order), on a compact host table [query users | 12 ctx | all items]."""
+    from oracle import cpu as ocpu
+    from oracle import parity
+    qc = Aq.shape[0]
+    if world == 1:
+        items = E[row0:row0 + ni].float().cpu()
+    else:                                   # rank 0 holds one shard: rebuild the catalog
+        items = torch.empty(ni, k, dtype=torch.float32)
+        step_ = 1 << 20
+        for b0 in range(0, ni, step_):
+            b1 = min(ni, b0 + step_)
+            items[b0:b1] = item_rows(b0, b1, k, dev).to(table_dtype).float().cpu()
+    Eh = torch.cat([check_rows.cpu(), items]).numpy()
+    del items
+    Ah = Aq.cpu().numpy().astype(np.int64)
+    nu = 1 << 20
+    Ac = np.empty_like(Ah)
+    Ac[:, 0] = np.arange(qc)
+    Ac[:, 1] = 0
+    Ac[:, 2:] = qc + (Ah[:, 2:] - nu)
+    Ac = Ac.astype(np.int32)
+    base = qc + 12
+    t0 = time.perf_counter()
+    rs, ri = ocpu.catalog_topk(Ac, Eh, 1, 20, base, ni, ctx=(2, 5), threads=_oracle_threads())
+    par = _topk_parity(s.cpu().numpy(), i.cpu().numpy(), ri, parity.hhfm_exact(Ac, Eh, base))
+    par["oracle"] = (f"oracle/cpu_oracle.c oracle_catalog_topk mode 1 over all {ni:,} items, "
+                     f"first {qc} queries, {_oracle_threads()} threads")
+    par["oracle_s"] = time.perf_counter() - t0
+    return par
+
+
+def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
     """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137),
     Frappe vocabulary, `rows` rows per GPU (12.5M = the 100M-row job over 8
     GPUs; weak scaling, rows sharded, no collective).  mlp=bf16: the fused
@@ -443,6 +562,7 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     ms = float(t[0]) / reps * 1e3
     kern = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    par = _c5_parity(m, X, out, mlp) if check else None
     fl = 2.0 * (5 * 256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)
     if mlp == torch.bfloat16:
         # executed (AUTO = ITEM): the projection of the M table rows for the 4
@@ -457,10 +577,17 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
                             f"Frappe vocabulary, rows sharded {rows:,} per GPU", "ranks": world,
                 "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
                 "executed_TFLOPs": ex / (kern * 1e-3) / 1e12,
-                "roofline": {"bound": "mfma", "flops_per_row": fl,
-                             "achieved_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
+                "roofline": {"bound": "mfma", "executed_flops_per_pass": ex,
+                             "achieved_TFLOPs": ex / (kern * 1e-3) / 1e12,
                              "peak_TFLOPs": 2500.0,
-                             "frac": fl * rows / (kern * 1e-3) / 1e12 / 2500.0}}
+                             "frac": ex / (kern * 1e-3) / 1e12 / 2500.0,
+                             "reference_flops_per_row": fl,
+                             "effective_TFLOPs": fl * rows / (kern * 1e-3) / 1e12,
+                             "effective_frac": fl * rows / (kern * 1e-3) / 1e12 / 2500.0,
+                             "note": "frac = FLOPs executed (projection + item field of layer "
+                                     "0 + hidden layers) / time / bf16 peak; effective_frac "
+                                     "prices the reference's 1.665 MFLOP/row"},
+                "parity": par}
     # executed FLOPs of the projected path: the per-call projection of the
     # M table rows (5 GEMMs [M,256]x[256,400]) + the hidden layers per row
     ex = 2.0 * 5 * M * 256 * 400 + rows * (2.0 * 2 * 400 * 400 + 2.0 * (5 * 416 + 256 + 400))
@@ -473,7 +600,45 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16):
             "roofline": {"bound": "mfma", "executed_flops_per_pass": ex,
                          "achieved_TFLOPs": ex / (kern * 1e-3) / 1e12,
                          "peak_TFLOPs": 157.3,
-                         "frac": ex / (kern * 1e-3) / 1e12 / 157.3}}
+                         "frac": ex / (kern * 1e-3) / 1e12 / 157.3},
+            "parity": par}
+
+
+C5_CHECK_ROWS = 1 << 16
+
+
+def _c5_parity(m, X, out, mlp):
+    """The first 65,536 rows of the timed pass against the oracle: the fp32
+    MLP against DFM.py:104-137 restated in fp32 (oracle/fm_oracle.dfm_out),
+    2e-5 of the output's magnitude Σ|concat_j·Wp_j| + |bp|; the bf16 MLP
+    against the oracle that rounds the same operands to bf16
+    (oracle/parity.dfm_bf16_out), 5e-3 of it (tests/test_gpu_dfm.py)."""
+    from oracle import fm_oracle as orc
+    from oracle import parity
+    n = min(C5_CHECK_ROWS, X.shape[0])
+    Xh = X[:n].cpu().numpy()
+    got = out[:n].cpu().numpy().astype(np.float64)
+    W = m.get_weights()
+    L = len(m.deep_layers)
+    Ls = [W[f"layer_{j}"] for j in range(L)]
+    Bs = [W[f"bias_{j}"] for j in range(L)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    t0 = time.perf_counter()
+    if m.table_dtype == torch.bfloat16:
+        E = parity.bf16_round(E)
+    mag = parity.dfm_magnitude(Xh, E, w, Ls, Bs, Wp, bp)
+    if mlp == torch.bfloat16:
+        ref = parity.dfm_bf16_out(Xh, E, w, Ls, Bs, Wp, bp)
+        tol, how = 5e-3, "oracle/parity.dfm_bf16_out (bf16-rounded operands)"
+    else:
+        ref = orc.dfm_out(Xh, E, w, Ls, Bs, Wp, bp)[:, 0]
+        tol, how = 2e-5, "oracle/fm_oracle.dfm_out (fp32, DFM.py:104-137)"
+    err = np.abs(got - ref) / mag
+    return {"rows": n, "oracle": how, "tolerance_of_magnitude": tol,
+            "max_err_of_magnitude": float(err.max()),
+            "rows_failing": int((err > tol).sum()), "parity": bool((err <= tol).all()),
+            "oracle_s": time.perf_counter() - t0}
 
 
 def stream_read_peak(buf, reps=5):
@@ -644,10 +809,11 @@ def main():
     del idx, E, w, out
     torch.cuda.empty_cache()
     extra = {}
+    check = not args.no_check
     # the extra legs never cost the headline line: a failure is recorded, not raised
     if "catalog" in legs:
         try:
-            extra["catalog_c4"] = catalog_leg(dev, world, rank)
+            extra["catalog_c4"] = catalog_leg(dev, world, rank, check=check)
         except Exception as e:  # noqa: BLE001
             extra["catalog_c4"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
@@ -658,18 +824,20 @@ def main():
             extra["catalog_c3"] = {"error": f"{type(e).__name__}: {e}"}
     if "catalog_bf16" in legs:
         try:
-            extra["catalog_c4_bf16"] = catalog_leg(dev, world, rank, table_dtype=torch.bfloat16)
+            extra["catalog_c4_bf16"] = catalog_leg(dev, world, rank, table_dtype=torch.bfloat16,
+                                                   check=check)
         except Exception as e:  # noqa: BLE001
             extra["catalog_c4_bf16"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
     if "c5" in legs:
         try:
-            extra["dfm_c5"] = c5_leg(dev, world, rank, args.c5_rows)
+            extra["dfm_c5"] = c5_leg(dev, world, rank, args.c5_rows, check=check and rank == 0)
         except Exception as e:  # noqa: BLE001
             extra["dfm_c5"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
         try:
-            extra["dfm_c5_f32"] = c5_leg(dev, world, rank, args.c5_rows, mlp=torch.float32)
+            extra["dfm_c5_f32"] = c5_leg(dev, world, rank, args.c5_rows, mlp=torch.float32,
+                                         check=check and rank == 0)
         except Exception as e:  # noqa: BLE001
             extra["dfm_c5_f32"] = {"error": f"{type(e).__name__}: {e}"}
         torch.cuda.empty_cache()
@@ -680,6 +848,21 @@ def main():
             extra["hr_at_10"] = {"error": f"{type(e).__name__}: {e}"}
     if extra:
         result["extra"] = extra
+    # one verdict per leg: True / False from the leg's oracle comparison, None
+    # when the leg did not run a check (or failed before it)
+    summary = {}
+    if "cpu_baseline" in result:
+        summary["k1_rows"] = result["cpu_baseline"]["gpu_vs_float64"]["parity"]
+    for name, leg in extra.items():
+        if name == "hr_at_10":
+            summary[name] = leg.get("identical_to_oracle")
+        elif isinstance(leg.get("parity"), dict):
+            summary[name] = leg["parity"]["parity"]
+        else:
+            summary[name] = None
+        if "matches_n1" in leg:
+            summary[name + "_matches_n1"] = leg["matches_n1"]
+    result["parity"] = summary
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -13,6 +13,7 @@ import pytest
 import torch
 
 from oracle import fm_oracle as orc
+from oracle import parity
 from tests.helpers import bf16_round
 
 pytestmark = pytest.mark.gpu
@@ -26,36 +27,8 @@ def _model(d_or_shapes, mlp_dtype=torch.float32, table_dtype=torch.float32):
                   table_dtype=table_dtype)
 
 
-def _magnitude(X, E, w, layers, biases, Wp, bp):
-    """Σ_j |concat_j · Wp_j| + |bp| in float64 (natural scale of the output)."""
-    X = np.asarray(X, np.int64)
-    e = E[X].astype(np.float64)
-    y1 = w[X].astype(np.float64)
-    s = e.sum(1)
-    y2 = 0.5 * (s * s - (e * e).sum(1))
-    h = e.reshape(len(X), -1)
-    for Wl, bl in zip(layers, biases):
-        h = np.maximum(h @ Wl.astype(np.float64) + bl.astype(np.float64), 0)
-    cat = np.concatenate([y1, y2, h], 1)
-    return (np.abs(cat * Wp.reshape(1, -1))).sum(1) + abs(float(bp))
-
-
-def _bf16_oracle(X, E, w, layers, biases, Wp, bp):
-    """bf16 MLP mode: table rows, weights and stored hidden activations rounded
-    to bf16; accumulation and the final dot in fp32; FM part in fp32."""
-    X = np.asarray(X, np.int64)
-    e = E[X]
-    y1 = w[X]
-    s = e.sum(1, dtype=np.float32)
-    y2 = np.float32(0.5) * (s * s - (e * e).sum(1, dtype=np.float32))
-    h = bf16_round(e.reshape(len(X), -1))
-    L = len(layers)
-    for i, (Wl, bl) in enumerate(zip(layers, biases)):
-        h = np.maximum(h @ bf16_round(Wl) + bl, 0).astype(np.float32)
-        if i < L - 1:
-            h = bf16_round(h)
-    cat = np.concatenate([y1, y2, h], 1)
-    return (cat @ Wp.reshape(-1, 1))[:, 0] + np.float32(bp)
+_magnitude = parity.dfm_magnitude
+_bf16_oracle = parity.dfm_bf16_out
 
 
 def test_dfm_vs_reference_graph():

@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from oracle import fm_oracle as orc
-from tests.helpers import (bf16_round, fm_exact, hhfm_exact, synth_rows, table,
+from tests.helpers import (bf16_round, fm_exact, hhfm_exact, log_parity, synth_rows, table,
                            topk_tie_swaps)
 
 pytestmark = pytest.mark.gpu
@@ -78,6 +78,10 @@ def _elementwise_vs_exact(got, ref, X, E, w, w0, scale, kappa_max=100.0):
     rel_gpu = np.abs(got - ex) / np.maximum(np.abs(ex), 1e-300)
     rel_ora = np.abs(ref - ex) / np.maximum(np.abs(ex), 1e-300)
     ok = kappa <= kappa_max
+    log_parity("fm_rows_kappa", rows=int(ok.size), rows_kappa_gt_100=int((~ok).sum()),
+               max_rel_err_kappa_le_100=float(rel_gpu[ok].max()),
+               max_rel_err_kappa_gt_100=float(rel_gpu[~ok].max()) if (~ok).any() else 0.0,
+               oracle_max_rel_err_kappa_gt_100=float(rel_ora[~ok].max()) if (~ok).any() else 0.0)
     assert rel_gpu[ok].max() <= RTOL, rel_gpu[ok].max()
     if (~ok).any():
         print(f"{int((~ok).sum())} rows with κ > {kappa_max}: max rel err gpu "
