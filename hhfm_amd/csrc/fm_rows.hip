@@ -259,7 +259,11 @@ __global__ __launch_bounds__(256) void hybrid_rows_generic(
   bool bad = false;
   for (int64_t row = wave; row < B; row += nwave) {
     const int32_t* p = idx + row * (int64_t)ncols;
-    for (int c = lane; c < ncols; c += kWave) bad |= clamp_id(p[c], M) != p[c];
+    // only the columns the score reads (user, item, ctx, time), like
+    // check_query_ids_kernel: an unused column never raises
+    for (int c = lane; c < ncols; c += kWave)
+      if (c == ucol || c == icol || (c >= c0 && c < c1) || (c >= t0 && c < t1))
+        bad |= clamp_id(p[c], M) != p[c];
     float t = 0.f;
     for (int e = lane; e < k; e += kWave) {
       float h = val(p[ucol], e);

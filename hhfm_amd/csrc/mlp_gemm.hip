@@ -194,6 +194,15 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
   return p;
 }
 
+// The fused kernels stream Wt by 16-B LDS-DMA (dfm_fused_launch declines a
+// misaligned view); a projected plan needs them, so a misaligned Wt plans
+// the direct path instead of failing after P was put on the stream.
+static bool wt_aligned(int32_t nlayers, const void* const* Wt) {
+  for (int i = 0; i < nlayers; ++i)
+    if (reinterpret_cast<uintptr_t>(Wt[i]) & 15) return false;
+  return true;
+}
+
 static bool proj_mode_ok(int m) {
   return m == HHFM_DFM_PROJ_OFF || m == HHFM_DFM_PROJ_ON || m == HHFM_DFM_PROJ_AUTO ||
          m == HHFM_DFM_PROJ_CTX || m == HHFM_DFM_PROJ_ITEM;
@@ -342,8 +351,9 @@ extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const 
   const int rc = dfm_forward_args(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
                                   bias, mlp_dtype, Wp, out);
   if (rc != 1) return rc;
-  // v3 behaviour: every field projected when the workspace holds that plan
-  DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, HHFM_DFM_PROJ_ON);
+  // AUTO (rows_total = B) when the workspace holds that plan, else direct
+  DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B,
+                       wt_aligned(nlayers, Wt) ? HHFM_DFM_PROJ_AUTO : HHFM_DFM_PROJ_OFF);
   if (!p.proj || !workspace || ws_bytes < p.total) p = dfm_plan(B, nlayers, layer_dims, mlp_dtype);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
@@ -362,6 +372,7 @@ extern "C" int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, con
   const int rc = dfm_forward_args(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
                                   bias, mlp_dtype, Wp, out);
   if (rc != 1) return rc;
+  if (!wt_aligned(nlayers, Wt)) proj_mode = HHFM_DFM_PROJ_OFF;
   const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
@@ -430,9 +441,10 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
   const int64_t qc = dfm_cat_qchunk(B, item_count, chunk_rows);
   const int64_t rows = qc * item_count;
   DfmPlan p;
-  if (proj_mode < 0) {   // legacy entry point: every field projected when the workspace holds it
+  if (!wt_aligned(nlayers, Wt)) proj_mode = HHFM_DFM_PROJ_OFF;
+  if (proj_mode < 0) {   // legacy entry point: AUTO when the workspace holds that plan
     p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                 B * (int64_t)item_count, HHFM_DFM_PROJ_ON, item_col, false);
+                 B * (int64_t)item_count, HHFM_DFM_PROJ_AUTO, item_col, false);
     if (!p.proj || !workspace || ws_bytes < dfm_cat_bytes(p, rows, F))
       p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
   } else {

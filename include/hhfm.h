@@ -183,10 +183,14 @@ int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int32_t* layer_
  * saving when rows >= 2·features_M (DFM.py:125-128 computed by the same
  * products, summed per field first).
  * The *_ex entry points take proj_mode explicitly; hhfm_dfm_forward /
- * hhfm_dfm_catalog_topk project every field when ws_bytes covers that plan
- * (the *_workspace_ex size with HHFM_DFM_PROJ_ON) and run direct otherwise.
+ * hhfm_dfm_catalog_topk follow HHFM_DFM_PROJ_AUTO when ws_bytes covers that
+ * plan (the *_workspace_ex size with HHFM_DFM_PROJ_AUTO) and run direct
+ * otherwise.  The plan (direct, projected, which fields) changes the
+ * summation order of layer 0, so scores may differ between plans within the
+ * tested tolerances (fp32 MLP 2e-5, bf16 MLP 5e-3 of the output magnitude).
  * Projection needs the fused envelope (k % 16 == 0, k <= 512, F <= 16,
- * <= 4 layers of <= 416 units); outside it every mode runs direct.
+ * <= 4 layers of <= 416 units) and 16-B aligned Wt[i]; otherwise every mode
+ * runs direct.
  * P needs (F - first projected field)·features_M·32·⌈max width/32⌉ floats
  * (at most 1 GiB planned). */
 enum hhfm_dfm_proj {

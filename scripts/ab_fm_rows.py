@@ -25,7 +25,7 @@ st = torch.cuda.current_stream().cuda_stream
 
 def run(v):
     nat.fm_score_rows_ex(idx.data_ptr(), rows, 5, E.data_ptr(), M, 64, 0, w.data_ptr(), 0.0,
-                         outs[v].data_ptr(), v, st)
+                         outs[v].data_ptr(), v, 0, st)
 
 
 for v in variants:

@@ -289,3 +289,43 @@ def test_dfm_catalog_item_column_permuted():
                                     dims, Wp, bp, 2, nu, ni, 20, 0, 1 << 20, proj=proj)
         bad, swaps = orc.topk_swaps(sc, ri, i.cpu().numpy(), tol)
         assert bad == 0 and swaps == 0, (proj, bad, swaps)
+
+
+def test_dfm_misaligned_weights_plan_direct():
+    """A Wt view that is 4-B but not 16-B aligned (the fused kernels' LDS-DMA
+    needs 16 B) makes AUTO plan the direct path instead of failing with
+    EUNSUPPORTED after P was computed (mlp_gemm.hip wt_aligned): the scores
+    equal the aligned call's direct-path scores within the fp32 tolerance."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(99)
+    nu, ni, F, k = 100, 200, 5, 64
+    M = nu + ni + 12
+    m = _model((nu, ni, M, F, k, [150, 200, 150]))
+    B = 4 * M                                       # AUTO projects (rows >= 2·M)
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    W = m.get_weights()
+    Ls = [W[f"layer_{i}"] for i in range(3)]
+    Bs = [W[f"bias_{i}"] for i in range(3)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    Wt, bs, dims, Wpd, bpd = m._prepared()
+    shifted = []
+    for t in Wt:
+        buf = torch.empty(t.numel() + 1, dtype=t.dtype, device=t.device)
+        v = buf[1:].view(t.shape)
+        v.copy_(t)
+        assert v.data_ptr() % 16 != 0
+        shifted.append(v)
+    xd = torch.from_numpy(X).cuda()
+    wb = m.weights["feature_bias"].reshape(-1)
+    got = ops.dfm_forward(xd, m.table, wb, shifted, bs, dims, torch.float32, Wpd, bpd,
+                          proj=None).cpu().numpy()
+    ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    assert np.all(np.abs(got - ref) <= 2e-5 * mag), np.max(np.abs(got - ref) / mag)
+    q = torch.from_numpy(X[:7]).cuda()
+    s, i = ops.dfm_catalog_topk(q, m.table, wb, shifted, bs, dims, Wpd, bpd, 1, nu, ni, 20, 0,
+                                1 << 20, proj=None)
+    s2, i2 = ops.dfm_catalog_topk(q, m.table, wb, Wt, bs, dims, Wpd, bpd, 1, nu, ni, 20, 0,
+                                  1 << 20, proj=False)
+    assert np.array_equal(i.cpu().numpy(), i2.cpu().numpy())

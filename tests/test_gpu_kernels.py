@@ -152,6 +152,25 @@ def test_hybrid_score_rows_parity(dtype, layout, k):
     assert np.all(np.abs(got - ref) <= RTOL * scale + 1e-12)
 
 
+def test_hybrid_generic_flags_only_read_columns():
+    """The generic row kernel (non-canonical layout: an extra column the score
+    never reads) flags bad ids only in the user, item, ctx and time columns,
+    like the catalog's query check and the reference's embedding_lookup."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(5)
+    X, M = synth_rows(rng, 999, 300, 900, (7, 2, 3))
+    E = table(rng, M, 64)
+    Xx = np.concatenate([X, np.full((len(X), 1), M + 5, np.int32)], 1)   # unused, out of range
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    got = ops.hybrid_score_rows(_dev(Xx), _dev(E), 0, 1, (2, 5), (0, 0), status=st)
+    assert int(st.item()) == 0
+    ref = orc.hhfm_positive_feedback(X, E, 3, 0)[:, 0]
+    assert np.allclose(got.cpu().numpy(), ref, rtol=0, atol=1e-7)
+    Xx[3, 4] = M + 1                                                     # a read column
+    ops.hybrid_score_rows(_dev(Xx), _dev(E), 0, 1, (2, 5), (0, 0), status=st)
+    assert int(st.item()) != 0
+
+
 def _hhfm_scale(A, E, n_user, n_item):
     """Per-query magnitude of h·item: max over items of Σ_k |h_k||i_k|."""
     h = np.abs(orc._hybrid(E, A[:, 0], A[:, 2:]).astype(np.float64))
@@ -386,8 +405,8 @@ def test_catalog_topk_c4_shard(dtype, monkeypatch):
 
 @pytest.mark.parametrize("exact", ["0", "1"])
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_catalog_topk_threshold_seed_is_exact(dtype, mode, exact, monkeypatch):
+@pytest.mark.parametrize("dtype,k", [("f32", 128), ("bf16", 64), ("bf16", 128)])
+def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact, monkeypatch):
     """The streaming path's threshold seed (exact top-K of the first 32,768
     items from the STORE score matrix) only drops items that cannot reach the
     top-K: seeded and unseeded runs return the same bits, and both match the
@@ -396,7 +415,7 @@ def test_catalog_topk_threshold_seed_is_exact(dtype, mode, exact, monkeypatch):
     from oracle import cpu as ocpu
     monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
     rng = np.random.default_rng(41)
-    nu, pre, N, k, B = 700, 333, 600_000, 128 if dtype == "f32" else 64, 300
+    nu, pre, N, B = 700, 333, 600_000, 300
     M = nu + pre + N + 12
     E = rng.standard_normal((M, k), dtype=np.float32) * np.float32(0.01)
     w = rng.normal(0, 0.01, M).astype(np.float32)
@@ -417,6 +436,17 @@ def test_catalog_topk_threshold_seed_is_exact(dtype, mode, exact, monkeypatch):
             res[seed] = (s.cpu().numpy(), i.cpu().numpy())
         assert np.array_equal(res["1"][0].view(np.int32), res["0"][0].view(np.int32))
         assert np.array_equal(res["1"][1], res["0"][1])
+        if K <= 32 and exact == "0" and k >= (128 if dtype == "bf16" else 64):
+            # catalog_ring (seeded, split-bf16, K <= 32) at 4 and 8 waves per
+            # workgroup: B = 300 leaves idle waves in the last query block
+            monkeypatch.setenv("HHFM_CATALOG_SEED", "1")
+            for waves in ("4", "8"):
+                monkeypatch.setenv("HHFM_RING_WAVES", waves)
+                s, i = ops.catalog_topk(_dev(A), Eg, m, K, nu + pre, N, 5000, wd, 0, (2, 5),
+                                        (0, 0))
+                assert np.array_equal(s.cpu().numpy().view(np.int32), res["1"][0].view(np.int32))
+                assert np.array_equal(i.cpu().numpy(), res["1"][1])
+            monkeypatch.delenv("HHFM_RING_WAVES")
         rs, ri = ocpu.catalog_topk(A, E, 0 if mode == "fm" else 1, K, nu + pre, N,
                                    w=w if mode == "fm" else None, ctx=(2, 5), threads=16)
         exact_fn = (fm_exact(A, E, w, nu + pre - 5000) if mode == "fm"
