@@ -54,7 +54,9 @@ HHFM_DEV float load_w(const float* __restrict__ w, int32_t id, int64_t M) {
   }
 }
 
-template <int F, int LPR, bool BF16, bool HAS_W, bool NT, int WAUX = -1>
+// PSTRIDE > 0: packed table, row m = [E[m] (LPR·16 B) | w[m] fp32 | pad] at a
+// row stride of PSTRIDE bytes (w read from the row, the `w` pointer unused).
+template <int F, int LPR, bool BF16, bool HAS_W, bool NT, int WAUX = -1, int PSTRIDE = 0>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
     int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out,
@@ -62,7 +64,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
   constexpr int U = RowsPerLane<F>::value;
   constexpr int RPW = kWave / LPR;  // rows per wave per unroll slot
   constexpr int RPI = RPW * U;      // rows per wave-iteration
-  constexpr int64_t ROW_BYTES = (int64_t)LPR * 16;
+  constexpr int64_t ROW_BYTES = PSTRIDE ? (int64_t)PSTRIDE : (int64_t)LPR * 16;
   using C = Chunk<BF16>;
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -103,7 +105,11 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
           int32_t my = id[u][0];
 #pragma unroll
           for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
-          const float wl = load_w<WAUX>(w, my, M);
+          float wl;
+          if constexpr (PSTRIDE > 0)
+            wl = *reinterpret_cast<const float*>(E + (int64_t)my * PSTRIDE + LPR * 16);
+          else
+            wl = load_w<WAUX>(w, my, M);
           wv[u] += (fsel < F) ? wl : 0.f;
         }
       }
@@ -322,6 +328,24 @@ static bool launch_fm_wpolicy(int sel, const int32_t* idx, int64_t B, const char
 #undef HHFM_WPOL
 }
 
+// Measurement variants: packed [E | w | pad] rows (flag bits 8..11: 1 = 272-B
+// stride, 2 = 384-B stride); the `w` argument is ignored, E is the packed table.
+static bool launch_fm_packed(int sel, const int32_t* idx, int64_t B, const char* E,
+                             int64_t M, float w0, float* out, int32_t* status,
+                             hipStream_t s) {
+  constexpr int RPB = 4 * (kWave / 16) * RowsPerLane<5>::value;
+  const int grid = grid_for(B, RPB);
+  if (sel == 1)
+    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, -1, 272>), dim3(grid),
+                       dim3(256), 0, s, idx, B, E, M, nullptr, w0, out, status);
+  else if (sel == 2)
+    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, -1, 384>), dim3(grid),
+                       dim3(256), 0, s, idx, B, E, M, nullptr, w0, out, status);
+  else
+    return false;
+  return true;
+}
+
 template <int F, int LPR, bool BF16>
 static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            int64_t M, const float* w, float w0, float* out,
@@ -420,6 +444,11 @@ extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
   const int lpr = lpr_for(k, dtype);
   const bool aligned = (reinterpret_cast<uintptr_t>(E) & 15) == 0;
   const int wsel = (flags >> 4) & 15;
+  const int psel = (flags >> 8) & 15;
+  if (psel && F == 5 && lpr == 16 && !bf16 && aligned &&
+      launch_fm_packed(psel, idx, B, reinterpret_cast<const char*>(E), features_M, w0, out,
+                       status, s))
+    return (int)hipGetLastError();
   if (wsel && F == 5 && lpr == 16 && !bf16 && aligned && w && features_M < (1LL << 29) &&
       launch_fm_wpolicy(wsel, idx, B, reinterpret_cast<const char*>(E), features_M, w, w0,
                         out, status, s))
