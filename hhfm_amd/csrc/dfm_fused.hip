@@ -92,6 +92,8 @@ struct FusedDfmArgs {
   // fp32 kernel takes the identity and no order.
   uint64_t perm;
   const int32_t* order;
+  // dfm_fused_f32s: base[m] = (Σ_f w·Wp + FM part) + bp from dfm_fm_base
+  const float* fmbase;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -947,13 +949,267 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
     }
   part += __shfl_xor(part, 16, kWave);
   part += __shfl_xor(part, 32, kWave);
+  const int64_t m = m0 + myrow;
   y2 += __shfl_xor(y2, 16, kWave);
   y2 += __shfl_xor(y2, 32, kWave);
-  const int64_t m = m0 + myrow;
   if (kq == 0 && m < a.B) {
     float y1 = 0.f;
     for (int f = 0; f < F; ++f) y1 += a.w[ids[myrow * F + f]] * wpl[f];
     a.out[m] = ((y1 + y2) + a.bp) + part;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp32 MLP with the hidden layers on split-bf16 MFMA (PROJ only: layer 0 is
+// the fp32 P gather above).  Every fp32 operand is split into three bf16
+// pieces, x = x0 + x1 + x2 exactly (split3x8), and each 32-k step of a
+// 16-unit output tile runs the six piece products of order >= 2^-16 on
+// v_mfma_f32_16x16x32_bf16, smallest first (w2x0, w1x1, w0x2, w1x0, w0x1,
+// w0x0): products exact in fp32, fp32 accumulation, the dropped products
+// below 2^-24 relative — fp32-faithful, the same contract as K2's split
+// kernels.  6 x 16 cycles per 32 k instead of 8 x 32 for 16x16x4_f32.
+//   * B operand: the layer input X stays fp32 in registers in the 16x16
+//     C/D layout (lane group kq holds units 16t + 4kq .. +3); a 32-k step c
+//     takes lane group kq's 8 k as {32c + 4kq .. +3, 32c + 16 + 4kq .. +3} —
+//     the k order inside a step is free as long as A uses the same — and
+//     splits them once per step for all 2·TM output tiles;
+//   * A operand: dfm_pack_weights_f32s pre-splits the weights once per call
+//     into half-chunks [piece][16·TM rows][kq][8 bf16] (one 32-k step, half
+//     the output units; a tile's fragment read is 1 KB contiguous), padded to
+//     a multiple of 4 KB so every wave issues the same number of LDS-DMAs;
+//   * a 3-slot LDS ring, filled two half-chunks ahead by lane-linear LDS-DMA;
+//     one counted vmcnt + s_barrier per half-chunk.
+// ---------------------------------------------------------------------------
+template <int TM>
+struct F32sCfg {
+  static constexpr int HR = 16 * TM;                          // rows of a half-chunk
+  static constexpr int PlaneB = HR * 64;                      // one piece plane
+  static constexpr int SlotB = (3 * PlaneB + 4095) / 4096 * 4096;
+  static constexpr int kDmaW = SlotB / 4096;                  // DMA instructions per wave
+};
+
+__host__ __device__ static inline int f32s_slot_bytes(int TM) { return (3 * 16 * TM * 64 + 4095) / 4096 * 4096; }
+
+__global__ __launch_bounds__(256) void dfm_pack_weights_f32s(FusedDfmArgs a, int TM,
+                                                             char* __restrict__ out) {
+  const int HR = 16 * TM, PlaneB = HR * 64, SlotB = f32s_slot_bytes(TM);
+  const int64_t total = (int64_t)(a.L - 1) * TM * 2 * HR * 4;
+  const float* const* Wf = reinterpret_cast<const float* const*>(a.Wt);
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int blk = (int)(x / (HR * 4));
+    const int rem = (int)(x - (int64_t)blk * HR * 4);
+    const int nl = rem >> 2, kq = rem & 3;
+    const int i = 1 + blk / (2 * TM), c = (blk >> 1) % TM, hh = blk & 1;
+    const int n = HR * hh + nl;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int kk = 32 * c + (j < 4 ? 4 * kq + j : 16 + 4 * kq + j - 4);
+      v[j] = (n < a.dims[i] && kk < a.ldb[i]) ? Wf[i][(int64_t)n * a.ldb[i] + kk] : 0.f;
+    }
+    bf16x8 p0, p1, p2;
+    split3x8(v, p0, p1, p2);
+    char* base = out + (int64_t)blk * SlotB + nl * 64 + kq * 16;
+    *reinterpret_cast<bf16x8*>(base) = p0;
+    *reinterpret_cast<bf16x8*>(base + PlaneB) = p1;
+    *reinterpret_cast<bf16x8*>(base + 2 * PlaneB) = p2;
+  }
+}
+
+template <bool TBF, int TM>
+__global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
+  using Cfg = F32sCfg<TM>;
+  constexpr int NR = TM * 32;
+  constexpr int T16 = 2 * TM;                // 16-unit output tiles
+  constexpr int kIds = 3 * Cfg::SlotB, kBl = kIds + kF32Rows * kFusedMaxF * 4;
+  constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
+  constexpr int kSmem = kWp + (kFusedMaxF + kFusedMaxK) * 4;
+  static_assert(kSmem <= kLdsBytes, "split fp32 DeepFM kernel: LDS");
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];   // ONE LDS object
+  int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
+  float* blv = reinterpret_cast<float*>(smem + kBl);
+  float* vl = reinterpret_cast<float*>(smem + kVl);
+  float* wpl = reinterpret_cast<float*>(smem + kWp);
+
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int r = l & 15, kq = l >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * kF32Rows;
+  const int F = a.F, k = a.k, L = a.L;
+  const int H = (L - 1) * TM * 2;            // hidden half-chunks
+
+  for (int x = tid; x < kF32Rows * F; x += 256) {
+    const int64_t m = m0 + x / F;
+    ids[x] = m < a.B ? clamp_id(a.idx[m * F + x % F], a.M) : 0;
+  }
+  for (int i = 0; i < L; ++i)
+    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
+  for (int x = tid; x < F + k; x += 256) wpl[x] = a.Wp[x];
+  __syncthreads();
+
+  // half-chunk hc -> ring slot: kDmaW lane-linear 1-KB DMAs per wave; past the
+  // last half-chunk the last one is re-read into the free slot, so every
+  // step issues the same count and the vmcnt wait below stays exact
+  auto dma_half = [&](int hc, int slot) {
+    const int blk = hc < H ? hc : H - 1;
+    const char* src = reinterpret_cast<const char*>(a.packed) + (int64_t)blk * Cfg::SlotB;
+    char* dst = smem + slot * Cfg::SlotB;
+#pragma unroll
+    for (int d = 0; d < Cfg::kDmaW; ++d) {
+      const int piece = wv + 4 * d;
+      lds_dma16(src + piece * 1024 + l * 16, dst + piece * 1024);
+    }
+  };
+  if (H > 0) {
+    dma_half(0, 0);
+    dma_half(1, 1);
+  }
+
+  // ----- layer 0 from P: acc = Σ_f P_f[x_f] (lane group kq: units 16t+4kq..+3) -----
+  const int myrow = 16 * wv + r;
+  f32x4 acc[T16];
+#pragma unroll
+  for (int t = 0; t < T16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < F; ++f) {
+    const float4* pp = reinterpret_cast<const float4*>(
+                           reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
+                           (int64_t)ids[myrow * F + f] * a.proj_ld) + kq;
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+      const float4 x = pp[4 * t];
+      acc[t][0] += x.x;
+      acc[t][1] += x.y;
+      acc[t][2] += x.z;
+      acc[t][3] += x.w;
+    }
+  }
+  // ----- hidden layers: 6 split-bf16 MFMAs per tile and 32-k step -----
+  auto mma = [](const bf16x8& w, const bf16x8& x, const f32x4& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);
+  };
+  f32x4 X[T16];
+  int hc = 0;
+  for (int i = 1; i < L; ++i) {
+    const float* bli = blv + (i - 1) * NR;
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)   // relu after every layer (DFM.py:128)
+        X[t][x] = fmaxf(acc[t][x] + bli[16 * t + 4 * kq + x], 0.f);
+      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int c = 0; c < TM; ++c) {
+      bf16x8 xb0, xb1, xb2;
+      {
+        const float v[8] = {X[2 * c][0],     X[2 * c][1],     X[2 * c][2],     X[2 * c][3],
+                            X[2 * c + 1][0], X[2 * c + 1][1], X[2 * c + 1][2], X[2 * c + 1][3]};
+        split3x8(v, xb0, xb1, xb2);
+      }
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh, ++hc) {
+        // this wave's DMA of half-chunk hc landed (hc+1's may still fly), every
+        // wave's reads of hc-1's slot are done: publish hc, refill hc-1's slot
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(Cfg::kDmaW)
+                     : "memory");
+        // half-chunk hc+2 into the slot hc-1 used: one DMA after each of the
+        // first kDmaW tiles (an LDS-DMA issue costs ~60 cycles; a burst of
+        // them would idle the MFMA pipe)
+        const int nb = hc + 2 < H ? hc + 2 : H - 1;
+        const char* dsrc = reinterpret_cast<const char*>(a.packed) + (int64_t)nb * Cfg::SlotB +
+                           wv * 1024 + l * 16;
+        char* ddst = smem + ((hc + 2) % 3) * Cfg::SlotB + wv * 1024;
+        const char* slot = smem + (hc % 3) * Cfg::SlotB + r * 64 + kq * 16;
+        auto frag = [&](int tl, int pc) {
+          return *reinterpret_cast<const bf16x8*>(slot + pc * Cfg::PlaneB + tl * 1024);
+        };
+        bf16x8 w0 = frag(0, 0), w1 = frag(0, 1), w2 = frag(0, 2);
+#pragma unroll
+        for (int tl = 0; tl < TM; ++tl) {
+          const bf16x8 c0 = w0, c1 = w1, c2 = w2;
+          if (tl + 1 < TM) {
+            w0 = frag(tl + 1, 0);
+            w1 = frag(tl + 1, 1);
+            w2 = frag(tl + 1, 2);
+          }
+          f32x4& ac = acc[TM * hh + tl];
+          ac = mma(c2, xb0, ac);   // smallest terms first
+          ac = mma(c1, xb1, ac);
+          ac = mma(c0, xb2, ac);
+          ac = mma(c1, xb0, ac);
+          ac = mma(c0, xb1, ac);
+          ac = mma(c0, xb0, ac);
+          if (tl < Cfg::kDmaW) lds_dma16(dsrc + tl * 4096, ddst + tl * 4096);
+        }
+#pragma unroll
+        for (int d = TM; d < Cfg::kDmaW; ++d) lds_dma16(dsrc + d * 4096, ddst + d * 4096);
+      }
+    }
+  }
+  dma_wait();   // the trailing (re-read) DMAs
+
+  const float* blL = blv + (L - 1) * NR;
+  float part = 0.f;
+#pragma unroll
+  for (int t = 0; t < T16; ++t)
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int n = 16 * t + 4 * kq + x;
+      part += fmaxf(acc[t][x] + blL[n], 0.f) * vl[n];
+    }
+  part += __shfl_xor(part, 16, kWave);
+  part += __shfl_xor(part, 32, kWave);
+  const int64_t m = m0 + myrow;
+  if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + part;
+}
+
+// base[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c ½((Σ_f e_fc)² − Σ_f e_fc²)·Wp[F+c]) + bp)
+// (DFM.py:109-122, 132-137 without the deep part): 16 lanes per row, 16-B
+// column chunks, at full occupancy — the FM part's table reads are latency-
+// bound inside the one-wave-per-SIMD MFMA kernel.
+template <bool TBF>
+__global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ idx, int64_t B,
+                                                   int F, const void* __restrict__ E, int64_t M,
+                                                   int k, const float* __restrict__ w,
+                                                   const float* __restrict__ Wp, float bp,
+                                                   float* __restrict__ base) {
+  const int l = threadIdx.x & 63, sub = l & 15;
+  const int64_t row0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
+  const int64_t nrow = ((int64_t)gridDim.x * blockDim.x) / 16;
+  for (int64_t m = row0; m < B; m += nrow) {   // a row's 16 lanes stay together
+    const int32_t* p = idx + m * F;
+    float y2 = 0.f;
+    for (int c0 = 4 * sub; c0 < k; c0 += 64) {
+      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = clamp_id(p[f], M);
+        float v[4];
+        if constexpr (TBF) {
+          const uint2 x = *reinterpret_cast<const uint2*>(
+              reinterpret_cast<const uint16_t*>(E) + id * k + c0);
+          v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+          v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+        } else {
+          const float4 x = *reinterpret_cast<const float4*>(
+              reinterpret_cast<const float*>(E) + id * k + c0);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          s4[x] += v[x];
+          q4[x] += v[x] * v[x];
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x) y2 += 0.5f * (s4[x] * s4[x] - q4[x]) * Wp[F + c0 + x];
+    }
+    y2 = group_sum<16>(y2);
+    if (sub == 0) {
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) y1 += w[clamp_id(p[f], M)] * Wp[f];
+      base[m] = (y1 + y2) + bp;
+    }
   }
 }
 
@@ -984,7 +1240,9 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16) {
   const int nc0 = mlp_bf16 ? (kFusedMaxF * kFusedMaxK / 16 + 3) / 4
                            : (kFusedMaxF * kFusedMaxK / 16 + 1) / 2;
   const int nch = mlp_bf16 ? (TM + 1) / 2 : TM;
-  return (size_t)(nc0 + (L - 1) * nch) * 32 * TM * 8 * 16;
+  const size_t direct = (size_t)(nc0 + (L - 1) * nch) * 32 * TM * 8 * 16;
+  const size_t split = (size_t)(L - 1) * TM * 2 * f32s_slot_bytes(TM);   // dfm_fused_f32s
+  return mlp_bf16 || direct >= split ? direct : split;
 }
 
 // ---------------------------------------------------------------------------
@@ -1073,11 +1331,18 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
 // proj != nullptr: the layer-0 products of fields [proj_from, F) come from
 // dfm_project_layer0's workspace (PROJ kernels; the fp32 MLP projects all
 // fields, proj_from = 0).
+// HHFM_DFM_F32_EXACT=1: the projected fp32-MLP forward keeps its hidden layers
+// on exact-fp32 MFMA (dfm_fused_f32) instead of split-bf16 (dfm_fused_f32s)
+bool dfm_f32_split() {
+  const char* e = getenv("HHFM_DFM_F32_EXACT");
+  return !(e && e[0] == '1');
+}
+
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      uint64_t perm, const int32_t* order, hipStream_t st) {
+                      uint64_t perm, const int32_t* order, float* fm_base, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -1105,8 +1370,46 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
     // the fp32 kernel projects all fields, in the caller's order
-    if ((pj && proj_from != 0) || perm != kDfmIdentityPerm || order) return false;
+    const bool split = pj && L > 1 && dfm_f32_split();
+    // (the split kernel also takes rows grouped by user: out[order[m]])
+    if ((pj && proj_from != 0) || perm != kDfmIdentityPerm || (order && !split)) return false;
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
+    if (split) {
+      if (!fm_base) return false;
+      {
+        const int64_t rows_per_block = 256 / 16;
+        int64_t fb = (B + rows_per_block - 1) / rows_per_block;
+        if (fb > 8192) fb = 8192;
+        if (tbf)
+          hipLaunchKernelGGL(dfm_fm_base<true>, dim3((unsigned)fb), dim3(256), 0, st, idx, B, F,
+                             E, M, k, w, Wp, bp, fm_base);
+        else
+          hipLaunchKernelGGL(dfm_fm_base<false>, dim3((unsigned)fb), dim3(256), 0, st, idx, B, F,
+                             E, M, k, w, Wp, bp, fm_base);
+      }
+      a.fmbase = fm_base;
+      const int64_t units = (int64_t)(L - 1) * TM * 2 * 16 * TM * 4;
+      const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+      hipLaunchKernelGGL(dfm_pack_weights_f32s, dim3(pblocks), dim3(256), 0, st, a, TM,
+                         reinterpret_cast<char*>(pack_ws));
+#define HHFM_FUSED32S(T)                                                                   \
+  case T:                                                                                  \
+    if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T>), grid, dim3(256), 0, st, a);      \
+    else hipLaunchKernelGGL((dfm_fused_f32s<false, T>), grid, dim3(256), 0, st, a);         \
+    break;
+      switch (TM) {
+        HHFM_FUSED32S(2)
+        HHFM_FUSED32S(4)
+        HHFM_FUSED32S(5)
+        HHFM_FUSED32S(7)
+        HHFM_FUSED32S(8)
+        HHFM_FUSED32S(10)
+        HHFM_FUSED32S(13)
+        default: return false;
+      }
+#undef HHFM_FUSED32S
+      return true;
+    }
     const int nc0 = pj ? 0 : (F * (k / 16) + 1) / 2;
     const int64_t units = (int64_t)(nc0 + (L - 1) * TM) * 32 * TM * 8;
     const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);

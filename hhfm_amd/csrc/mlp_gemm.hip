@@ -30,13 +30,14 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      uint64_t perm, const int32_t* order, hipStream_t st);
+                      uint64_t perm, const int32_t* order, float* fm_base, hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
                         int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
                         const int32_t* dims, void* ws, hipStream_t st);
 size_t dfm_order_bytes(int64_t B, int F, int64_t M);
+bool dfm_f32_split();
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
                               void* ws, const int32_t** rows_out, hipStream_t st);
 constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
@@ -183,7 +184,14 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
       p.perm = perm;
       off += al256(pb);
       p.off_order = off;
-      if (mode == HHFM_DFM_PROJ_ITEM && forward && B <= 0x7fffffff) {
+      // fp32 MLP on the split kernel: rows grouped by user too (a block then
+      // reads one or two users' P rows: L1/L2 hits instead of Infinity-Cache
+      // reads); HHFM_DFM_F32_GROUP=0 turns it off
+      const char* ge = getenv("HHFM_DFM_F32_GROUP");
+      const bool f32_group_env = !(ge && ge[0] == '0');
+      const bool f32_group = !bf && mode == HHFM_DFM_PROJ_ON && forward && nlayers > 1 &&
+                             rows_total >= 64 * M && f32_group_env && dfm_f32_split();
+      if (((mode == HHFM_DFM_PROJ_ITEM) || f32_group) && forward && B <= 0x7fffffff) {
         p.group = true;
         off += al256(dfm_order_bytes(B, F, M));
       }
@@ -237,7 +245,8 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
   }();
   if ((proj || !layered) && p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
-                       Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order, st))
+                       Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order,
+                       reinterpret_cast<float*>(ws + p.off_base), st))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);

@@ -329,3 +329,46 @@ def test_dfm_misaligned_weights_plan_direct():
     s2, i2 = ops.dfm_catalog_topk(q, m.table, wb, Wt, bs, dims, Wpd, bpd, 1, nu, ni, 20, 0,
                                   1 << 20, proj=False)
     assert np.array_equal(i.cpu().numpy(), i2.cpu().numpy())
+
+
+@pytest.mark.parametrize("tdt", ["f32", "bf16"])
+def test_dfm_f32_split_grouped(tdt, monkeypatch):
+    """fp32 MLP, projected layer 0, hidden layers on split-bf16 MFMA
+    (dfm_fused_f32s) with the rows grouped by user (rows >= 64 x table rows):
+    within the fp32 tolerance of the reference graph, equal to the ungrouped
+    call up to summation order, and a row's score independent of its block
+    (a permuted batch gives the permuted scores bit for bit)."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(64)
+    F, k, M, users, B = 5, 64, 997, 40, 70000
+    tdtype = torch.bfloat16 if tdt == "bf16" else torch.float32
+    m = _model((users, 400, M, F, k, [150, 200, 150]), table_dtype=tdtype)
+    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    X[:, 0] = rng.integers(0, users, B)
+    W = m.get_weights()
+    Ls = [W[f"layer_{i}"] for i in range(3)]
+    Bs = [W[f"bias_{i}"] for i in range(3)]
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    if tdt == "bf16":
+        E = bf16_round(E)
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    Wt, bs, dims, Wpd, bpd = m._prepared()
+    wb = m.weights["feature_bias"].reshape(-1)
+    xd = torch.from_numpy(X).cuda()
+    got = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                          proj=True).cpu().numpy()
+    perm = rng.permutation(B)
+    again = ops.dfm_forward(xd[torch.from_numpy(perm).cuda()], m.table, wb, Wt, bs, dims,
+                            torch.float32, Wpd, bpd, proj=True).cpu().numpy()
+    monkeypatch.setenv("HHFM_DFM_F32_GROUP", "0")
+    flat = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                           proj=True).cpu().numpy()
+    monkeypatch.setenv("HHFM_DFM_F32_EXACT", "1")
+    exact = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                            proj=True).cpu().numpy()
+    ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    for name, v in (("grouped", got), ("ungrouped", flat), ("exact", exact)):
+        err = np.abs(v - ref) / mag
+        assert np.all(err <= 2e-5), (name, float(err.max()))
+    assert np.array_equal(again, got[perm])
