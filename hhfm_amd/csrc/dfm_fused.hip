@@ -54,6 +54,8 @@ namespace hhfm {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
+bool dfm_f32_split();
+
 constexpr int kFusedMaxLayers = 4;
 constexpr int kFusedMaxF = 16;
 constexpr int kFusedMaxK = 512;
@@ -974,21 +976,25 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32(FusedDfmArgs a) {
 //     the k order inside a step is free as long as A uses the same — and
 //     splits them once per step for all 2·TM output tiles;
 //   * A operand: dfm_pack_weights_f32s pre-splits the weights once per call
-//     into half-chunks [piece][16·TM rows][kq][8 bf16] (one 32-k step, half
-//     the output units; a tile's fragment read is 1 KB contiguous), padded to
+//     into half-chunks [piece][tile][kq][16 rows][8 bf16] (one 32-k step,
+//     half the output units; a tile's fragment read is 1 KB contiguous and
+//     each 16-lane group reads 256 consecutive bytes), padded to
 //     a multiple of 4 KB so every wave issues the same number of LDS-DMAs;
 //   * a 3-slot LDS ring, filled two half-chunks ahead by lane-linear LDS-DMA;
 //     one counted vmcnt + s_barrier per half-chunk.
 // ---------------------------------------------------------------------------
-template <int TM>
+template <int TM, int NW>
 struct F32sCfg {
   static constexpr int HR = 16 * TM;                          // rows of a half-chunk
   static constexpr int PlaneB = HR * 64;                      // one piece plane
-  static constexpr int SlotB = (3 * PlaneB + 4095) / 4096 * 4096;
-  static constexpr int kDmaW = SlotB / 4096;                  // DMA instructions per wave
+  static constexpr int SlotB = (3 * PlaneB + 8191) / 8192 * 8192;
+  static constexpr int kDmaW = SlotB / (1024 * NW);           // DMA instructions per wave
+  static constexpr int kRows = 16 * NW;                       // rows per workgroup
 };
 
-__host__ __device__ static inline int f32s_slot_bytes(int TM) { return (3 * 16 * TM * 64 + 4095) / 4096 * 4096; }
+__host__ __device__ static inline int f32s_slot_bytes(int TM) {
+  return (3 * 16 * TM * 64 + 8191) / 8192 * 8192;
+}
 
 __global__ __launch_bounds__(256) void dfm_pack_weights_f32s(FusedDfmArgs a, int TM,
                                                              char* __restrict__ out) {
@@ -1010,42 +1016,47 @@ __global__ __launch_bounds__(256) void dfm_pack_weights_f32s(FusedDfmArgs a, int
     }
     bf16x8 p0, p1, p2;
     split3x8(v, p0, p1, p2);
-    char* base = out + (int64_t)blk * SlotB + nl * 64 + kq * 16;
+    // [piece][tile][kq][row in tile] x 16 B: the 16 lanes of one kq read 256
+    // consecutive bytes (conflict-free ds_read_b128)
+    char* base = out + (int64_t)blk * SlotB + (nl >> 4) * 1024 + kq * 256 + (nl & 15) * 16;
     *reinterpret_cast<bf16x8*>(base) = p0;
     *reinterpret_cast<bf16x8*>(base + PlaneB) = p1;
     *reinterpret_cast<bf16x8*>(base + 2 * PlaneB) = p2;
   }
 }
 
-template <bool TBF, int TM>
-__global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
-  using Cfg = F32sCfg<TM>;
+// NW waves x 16 rows per workgroup: 8 waves (two per SIMD, 128 rows) halve
+// the weight bytes per row against 4 and let one wave's LDS-DMA issue and
+// barrier wait overlap the other's MFMAs; each wave keeps acc (104) + X (104)
+// within the 256 registers two waves per SIMD leave it.
+template <bool TBF, int TM, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
+  using Cfg = F32sCfg<TM, NW>;
   constexpr int NR = TM * 32;
   constexpr int T16 = 2 * TM;                // 16-unit output tiles
-  constexpr int kIds = 3 * Cfg::SlotB, kBl = kIds + kF32Rows * kFusedMaxF * 4;
-  constexpr int kVl = kBl + kFusedMaxLayers * NR * 4, kWp = kVl + NR * 4;
-  constexpr int kSmem = kWp + (kFusedMaxF + kFusedMaxK) * 4;
+  constexpr int NT = NW * 64;
+  constexpr int kIds = 3 * Cfg::SlotB, kBl = kIds + Cfg::kRows * kFusedMaxF * 4;
+  constexpr int kVl = kBl + kFusedMaxLayers * NR * 4;
+  constexpr int kSmem = kVl + NR * 4;
   static_assert(kSmem <= kLdsBytes, "split fp32 DeepFM kernel: LDS");
   __shared__ __attribute__((aligned(16))) char smem[kSmem];   // ONE LDS object
   int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
   float* blv = reinterpret_cast<float*>(smem + kBl);
   float* vl = reinterpret_cast<float*>(smem + kVl);
-  float* wpl = reinterpret_cast<float*>(smem + kWp);
 
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int r = l & 15, kq = l >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * kF32Rows;
+  const int64_t m0 = (int64_t)blockIdx.x * Cfg::kRows;
   const int F = a.F, k = a.k, L = a.L;
   const int H = (L - 1) * TM * 2;            // hidden half-chunks
 
-  for (int x = tid; x < kF32Rows * F; x += 256) {
+  for (int x = tid; x < Cfg::kRows * F; x += NT) {
     const int64_t m = m0 + x / F;
     ids[x] = m < a.B ? clamp_id(a.idx[m * F + x % F], a.M) : 0;
   }
   for (int i = 0; i < L; ++i)
-    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
-  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
-  for (int x = tid; x < F + k; x += 256) wpl[x] = a.Wp[x];
+    for (int n = tid; n < NR; n += NT) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += NT) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
   __syncthreads();
 
   // half-chunk hc -> ring slot: kDmaW lane-linear 1-KB DMAs per wave; past the
@@ -1057,7 +1068,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     char* dst = smem + slot * Cfg::SlotB;
 #pragma unroll
     for (int d = 0; d < Cfg::kDmaW; ++d) {
-      const int piece = wv + 4 * d;
+      const int piece = wv + NW * d;
       lds_dma16(src + piece * 1024 + l * 16, dst + piece * 1024);
     }
   };
@@ -1066,11 +1077,12 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     dma_half(1, 1);
   }
 
-  // ----- layer 0 from P: acc = Σ_f P_f[x_f] (lane group kq: units 16t+4kq..+3) -----
+  // ----- layer 0 from P: X = Σ_f P_f[x_f] (lane group kq: units 16t+4kq..+3),
+  // straight into the registers of layer 1's input -----
   const int myrow = 16 * wv + r;
-  f32x4 acc[T16];
+  f32x4 X[T16];
 #pragma unroll
-  for (int t = 0; t < T16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < T16; ++t) X[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int f = 0; f < F; ++f) {
     const float4* pp = reinterpret_cast<const float4*>(
                            reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
@@ -1078,27 +1090,25 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
 #pragma unroll
     for (int t = 0; t < T16; ++t) {
       const float4 x = pp[4 * t];
-      acc[t][0] += x.x;
-      acc[t][1] += x.y;
-      acc[t][2] += x.z;
-      acc[t][3] += x.w;
+      X[t][0] += x.x;
+      X[t][1] += x.y;
+      X[t][2] += x.z;
+      X[t][3] += x.w;
     }
   }
   // ----- hidden layers: 6 split-bf16 MFMAs per tile and 32-k step -----
   auto mma = [](const bf16x8& w, const bf16x8& x, const f32x4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);
   };
-  f32x4 X[T16];
+  f32x4 acc[T16];
   int hc = 0;
   for (int i = 1; i < L; ++i) {
     const float* bli = blv + (i - 1) * NR;
 #pragma unroll
-    for (int t = 0; t < T16; ++t) {
+    for (int t = 0; t < T16; ++t)
 #pragma unroll
       for (int x = 0; x < 4; ++x)   // relu after every layer (DFM.py:128)
-        X[t][x] = fmaxf(acc[t][x] + bli[16 * t + 4 * kq + x], 0.f);
-      acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+        X[t][x] = fmaxf((i == 1 ? X[t][x] : acc[t][x]) + bli[16 * t + 4 * kq + x], 0.f);
 #pragma unroll
     for (int c = 0; c < TM; ++c) {
       bf16x8 xb0, xb1, xb2;
@@ -1120,30 +1130,47 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_f32s(FusedDfmArgs a) {
         const char* dsrc = reinterpret_cast<const char*>(a.packed) + (int64_t)nb * Cfg::SlotB +
                            wv * 1024 + l * 16;
         char* ddst = smem + ((hc + 2) % 3) * Cfg::SlotB + wv * 1024;
-        const char* slot = smem + (hc % 3) * Cfg::SlotB + r * 64 + kq * 16;
+        const char* slot = smem + (hc % 3) * Cfg::SlotB + kq * 256 + r * 16;
         auto frag = [&](int tl, int pc) {
           return *reinterpret_cast<const bf16x8*>(slot + pc * Cfg::PlaneB + tl * 1024);
         };
-        bf16x8 w0 = frag(0, 0), w1 = frag(0, 1), w2 = frag(0, 2);
+        // fragments one tile ahead at one wave per SIMD; at two the other
+        // wave covers the LDS latency and the registers go to acc + X
+        constexpr bool kAhead = NW == 4;
+        bf16x8 w0, w1, w2;
+        if constexpr (kAhead) {
+          w0 = frag(0, 0);
+          w1 = frag(0, 1);
+          w2 = frag(0, 2);
+        }
 #pragma unroll
         for (int tl = 0; tl < TM; ++tl) {
-          const bf16x8 c0 = w0, c1 = w1, c2 = w2;
-          if (tl + 1 < TM) {
-            w0 = frag(tl + 1, 0);
-            w1 = frag(tl + 1, 1);
-            w2 = frag(tl + 1, 2);
+          bf16x8 c0, c1, c2;
+          if constexpr (kAhead) {
+            c0 = w0; c1 = w1; c2 = w2;
+            if (tl + 1 < TM) {
+              w0 = frag(tl + 1, 0);
+              w1 = frag(tl + 1, 1);
+              w2 = frag(tl + 1, 2);
+            }
+          } else {
+            c0 = frag(tl, 0);
+            c1 = frag(tl, 1);
+            c2 = frag(tl, 2);
           }
           f32x4& ac = acc[TM * hh + tl];
-          ac = mma(c2, xb0, ac);   // smallest terms first
+          // smallest terms first; a layer's first step starts from zero
+          ac = mma(c2, xb0, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ac);
           ac = mma(c1, xb1, ac);
           ac = mma(c0, xb2, ac);
           ac = mma(c1, xb0, ac);
           ac = mma(c0, xb1, ac);
           ac = mma(c0, xb0, ac);
-          if (tl < Cfg::kDmaW) lds_dma16(dsrc + tl * 4096, ddst + tl * 4096);
+          if (tl < Cfg::kDmaW) lds_dma16(dsrc + tl * NW * 1024, ddst + tl * NW * 1024);
         }
 #pragma unroll
-        for (int d = TM; d < Cfg::kDmaW; ++d) lds_dma16(dsrc + d * 4096, ddst + d * 4096);
+        for (int d = TM; d < Cfg::kDmaW; ++d)
+          lds_dma16(dsrc + d * NW * 1024, ddst + d * NW * 1024);
       }
     }
   }
@@ -1179,11 +1206,22 @@ __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ i
   const int64_t nrow = ((int64_t)gridDim.x * blockDim.x) / 16;
   for (int64_t m = row0; m < B; m += nrow) {   // a row's 16 lanes stay together
     const int32_t* p = idx + m * F;
-    float y2 = 0.f;
-    for (int c0 = 4 * sub; c0 < k; c0 += 64) {
-      float s4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int f = 0; f < F; ++f) {
-        const int64_t id = clamp_id(p[f], M);
+    // lane `sub` owns columns 64j + 4sub .. +3 (j < k/64): every field's
+    // loads of the row are independent, two fields in flight at a time
+    constexpr int kJ = kFusedMaxK / 64;
+    float s4[kJ][4], q4[kJ][4];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) { s4[j][x] = 0.f; q4[j][x] = 0.f; }
+#pragma unroll 2
+    for (int f = 0; f < F; ++f) {
+      const int64_t id = clamp_id(p[f], M);
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const int c0 = 64 * j + 4 * sub;
+        if (64 * j >= k) break;
+        if (c0 >= k) continue;   // k % 64 != 0: the last block is partial
         float v[4];
         if constexpr (TBF) {
           const uint2 x = *reinterpret_cast<const uint2*>(
@@ -1197,12 +1235,19 @@ __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ i
         }
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
-          s4[x] += v[x];
-          q4[x] += v[x] * v[x];
+          s4[j][x] += v[x];
+          q4[j][x] += v[x] * v[x];
         }
       }
+    }
+    float y2 = 0.f;
 #pragma unroll
-      for (int x = 0; x < 4; ++x) y2 += 0.5f * (s4[x] * s4[x] - q4[x]) * Wp[F + c0 + x];
+    for (int j = 0; j < kJ; ++j) {
+      if (64 * j >= k) break;
+      if (64 * j + 4 * sub >= k) continue;
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        y2 += 0.5f * (s4[j][x] * s4[j][x] - q4[j][x]) * Wp[F + 64 * j + 4 * sub + x];
     }
     y2 = group_sum<16>(y2);
     if (sub == 0) {
@@ -1337,6 +1382,13 @@ bool dfm_f32_split() {
   const char* e = getenv("HHFM_DFM_F32_EXACT");
   return !(e && e[0] == '1');
 }
+// waves per workgroup of the split kernel: 8 (128 rows, default) or 4
+// (HHFM_DFM_F32_WAVES=4, 64 rows, one wave per SIMD)
+static int dfm_f32_waves() {
+  const char* e = getenv("HHFM_DFM_F32_WAVES");
+  return e && e[0] == '4' ? 4 : 8;
+}
+
 
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
@@ -1392,10 +1444,17 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
       const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
       hipLaunchKernelGGL(dfm_pack_weights_f32s, dim3(pblocks), dim3(256), 0, st, a, TM,
                          reinterpret_cast<char*>(pack_ws));
+      const bool w8 = dfm_f32_waves() == 8;
+      const dim3 g8((unsigned)((B + 127) / 128));
 #define HHFM_FUSED32S(T)                                                                   \
   case T:                                                                                  \
-    if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T>), grid, dim3(256), 0, st, a);      \
-    else hipLaunchKernelGGL((dfm_fused_f32s<false, T>), grid, dim3(256), 0, st, a);         \
+    if (w8) {                                                                              \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T, 8>), g8, dim3(512), 0, st, a);   \
+      else hipLaunchKernelGGL((dfm_fused_f32s<false, T, 8>), g8, dim3(512), 0, st, a);      \
+    } else {                                                                               \
+      if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T, 4>), grid, dim3(256), 0, st, a); \
+      else hipLaunchKernelGGL((dfm_fused_f32s<false, T, 4>), grid, dim3(256), 0, st, a);    \
+    }                                                                                      \
     break;
       switch (TM) {
         HHFM_FUSED32S(2)

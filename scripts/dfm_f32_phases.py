@@ -44,14 +44,15 @@ for c in (7, 2, 3):
     off += c
 X = torch.stack(cols, 1).to(torch.int32).contiguous()
 res = {"rows": B}
-for grp in ("1", "0"):
+for grp, waves in (("1", "8"), ("1", "4"), ("0", "8")):
     os.environ["HHFM_DFM_F32_GROUP"] = grp
+    os.environ["HHFM_DFM_F32_WAVES"] = waves
     for layers in ([400, 400], [400, 400, 400]):
         m = DeepFM(nu, ni, M, 5, 256, layers, None, 0.01, 0, 0.0, device=dev)
         Wt, bs, dims, Wp, bp = m._prepared()
         out = torch.empty(B, device=dev)
         wb = m.weights["feature_bias"].reshape(-1)
-        res[f"group{grp}_L{len(layers)}"] = timeit(
+        res[f"group{grp}_w{waves}_L{len(layers)}"] = timeit(
             lambda: ops.dfm_forward(X, m.table, wb, Wt, bs, dims, torch.float32, Wp, bp, out=out,
                                     proj=True))
 print(json.dumps(res), flush=True)
