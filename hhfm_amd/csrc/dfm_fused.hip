@@ -94,8 +94,10 @@ struct FusedDfmArgs {
   // fp32 kernel takes the identity and no order.
   uint64_t perm;
   const int32_t* order;
-  // dfm_fused_f32s: base[m] = (Σ_f w·Wp + FM part) + bp from dfm_fm_base
+  // dfm_fused_f32s: base[m] = (Σ_f w·Wp + FM part) + bp from dfm_fm_base;
+  // stage: P rows of narrow-span fields staged in LDS (HHFM_DFM_F32_STAGE=0: off)
   const float* fmbase;
+  int stage;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -1037,12 +1039,20 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   constexpr int NT = NW * 64;
   constexpr int kIds = 3 * Cfg::SlotB, kBl = kIds + Cfg::kRows * kFusedMaxF * 4;
   constexpr int kVl = kBl + kFusedMaxLayers * NR * 4;
-  constexpr int kSmem = kVl + NR * 4;
+  constexpr int kSpan = kVl + NR * 4;        // [F] lo, [F] hi, [F] staged row base
+  constexpr int kSmem = kSpan + 3 * kFusedMaxF * 4;
   static_assert(kSmem <= kLdsBytes, "split fp32 DeepFM kernel: LDS");
+  // P rows staged in ring slot 2 (free until the first hidden half-chunk),
+  // padded by one 16-B chunk per row against bank conflicts
+  constexpr int kPRowB = NR * 4 + 16;
+  constexpr int kStageRows = Cfg::SlotB / kPRowB;
   __shared__ __attribute__((aligned(16))) char smem[kSmem];   // ONE LDS object
   int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
   float* blv = reinterpret_cast<float*>(smem + kBl);
   float* vl = reinterpret_cast<float*>(smem + kVl);
+  int32_t* plo = reinterpret_cast<int32_t*>(smem + kSpan);
+  int32_t* phi = plo + kFusedMaxF;
+  int32_t* psb = phi + kFusedMaxF;
 
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int r = l & 15, kq = l >> 4;
@@ -1057,6 +1067,51 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   for (int i = 0; i < L; ++i)
     for (int n = tid; n < NR; n += NT) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
   for (int n = tid; n < NR; n += NT) vl[n] = n < a.dims[L - 1] ? a.Wp[F + k + n] : 0.f;
+  if (tid < F) {
+    plo[tid] = 0x7fffffff;
+    phi[tid] = -1;
+  }
+  __syncthreads();
+  // each field's id span over the block (rows grouped by user: the user and
+  // the context fields span a few table rows)
+  for (int x = tid; x < Cfg::kRows * F; x += NT) {
+    const int64_t m = m0 + x / F;
+    if (m < a.B) {
+      atomicMin(&plo[x % F], ids[x]);
+      atomicMax(&phi[x % F], ids[x]);
+    }
+  }
+  __syncthreads();
+  // staging plan (every thread computes the same): fields in order, while
+  // their spans fit the slot's kStageRows rows
+  int staged = 0;
+  for (int f = 0; f < F; ++f) {
+    const int span = phi[f] - plo[f] + 1;
+    const bool st = a.stage && span > 0 && staged + span <= kStageRows;
+    if (tid == 0) psb[f] = st ? staged : -1;
+    staged += st ? span : 0;
+  }
+  __syncthreads();
+  char* pstage = smem + 2 * Cfg::SlotB;
+  if (staged > 0) {
+    // lane-linear LDS-DMA: chunk c of the image = row c / CPR, 16-B part
+    // c % CPR (the last part of a row is padding: it re-reads part 0)
+    constexpr int CPR = kPRowB / 16;
+    const int nins = (staged * CPR + 63) / 64;
+    for (int ins = wv; ins < nins; ins += NW) {
+      const int c = ins * 64 + l;
+      const int row = c / CPR < staged ? c / CPR : 0;
+      const int part = c % CPR < CPR - 1 ? c % CPR : 0;
+      int f = 0;
+      for (int g = 0; g < F; ++g)
+        if (psb[g] >= 0 && row >= psb[g] && row <= psb[g] + phi[g] - plo[g]) f = g;
+      const int64_t id = plo[f] + (row - psb[f]);
+      const char* src = reinterpret_cast<const char*>(a.proj) +
+                        ((int64_t)f * a.proj_fstride + id * a.proj_ld) * 4 + part * 16;
+      lds_dma16(src, pstage + ins * 1024);
+    }
+    dma_wait();
+  }
   __syncthreads();
 
   // half-chunk hc -> ring slot: kDmaW lane-linear 1-KB DMAs per wave; past the
@@ -1084,16 +1139,31 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
 #pragma unroll
   for (int t = 0; t < T16; ++t) X[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int f = 0; f < F; ++f) {
-    const float4* pp = reinterpret_cast<const float4*>(
-                           reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
-                           (int64_t)ids[myrow * F + f] * a.proj_ld) + kq;
+    const int id = ids[myrow * F + f];
+    const int sb = psb[f];   // uniform: this field's rows staged in LDS
+    if (sb >= 0) {
+      const float4* pp = reinterpret_cast<const float4*>(
+                             pstage + (sb + id - plo[f]) * kPRowB) + kq;
 #pragma unroll
-    for (int t = 0; t < T16; ++t) {
-      const float4 x = pp[4 * t];
-      X[t][0] += x.x;
-      X[t][1] += x.y;
-      X[t][2] += x.z;
-      X[t][3] += x.w;
+      for (int t = 0; t < T16; ++t) {
+        const float4 x = pp[4 * t];
+        X[t][0] += x.x;
+        X[t][1] += x.y;
+        X[t][2] += x.z;
+        X[t][3] += x.w;
+      }
+    } else {
+      const float4* pp = reinterpret_cast<const float4*>(
+                             reinterpret_cast<const float*>(a.proj) + f * a.proj_fstride +
+                             (int64_t)id * a.proj_ld) + kq;
+#pragma unroll
+      for (int t = 0; t < T16; ++t) {
+        const float4 x = pp[4 * t];
+        X[t][0] += x.x;
+        X[t][1] += x.y;
+        X[t][2] += x.z;
+        X[t][3] += x.w;
+      }
     }
   }
   // ----- hidden layers: 6 split-bf16 MFMAs per tile and 32-k step -----
@@ -1195,7 +1265,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
 // (DFM.py:109-122, 132-137 without the deep part): 16 lanes per row, 16-B
 // column chunks, at full occupancy — the FM part's table reads are latency-
 // bound inside the one-wave-per-SIMD MFMA kernel.
-template <bool TBF>
+template <bool TBF, int KJ>
 __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ idx, int64_t B,
                                                    int F, const void* __restrict__ E, int64_t M,
                                                    int k, const float* __restrict__ w,
@@ -1204,50 +1274,51 @@ __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ i
   const int l = threadIdx.x & 63, sub = l & 15;
   const int64_t row0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
   const int64_t nrow = ((int64_t)gridDim.x * blockDim.x) / 16;
+  // lane `sub` owns columns 64j + 4sub .. +3: KJ = k / 64 independent 16-B
+  // loads per field (KJ = 0: any k % 4 == 0, one column block at a time)
+  constexpr int J = KJ > 0 ? KJ : 1;
   for (int64_t m = row0; m < B; m += nrow) {   // a row's 16 lanes stay together
     const int32_t* p = idx + m * F;
-    // lane `sub` owns columns 64j + 4sub .. +3 (j < k/64): every field's
-    // loads of the row are independent, two fields in flight at a time
-    constexpr int kJ = kFusedMaxK / 64;
-    float s4[kJ][4], q4[kJ][4];
+    float y2 = 0.f;
+    for (int c00 = 0; c00 < k; c00 += 64 * J) {
+      float s4[J][4], q4[J][4];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j)
+      for (int j = 0; j < J; ++j)
 #pragma unroll
-      for (int x = 0; x < 4; ++x) { s4[j][x] = 0.f; q4[j][x] = 0.f; }
-#pragma unroll 2
-    for (int f = 0; f < F; ++f) {
-      const int64_t id = clamp_id(p[f], M);
+        for (int x = 0; x < 4; ++x) { s4[j][x] = 0.f; q4[j][x] = 0.f; }
+      const bool live = KJ > 0 || c00 + 4 * sub < k;
+#pragma unroll 4
+      for (int f = 0; f < F; ++f) {
+        const int64_t id = clamp_id(p[f], M);
 #pragma unroll
-      for (int j = 0; j < kJ; ++j) {
-        const int c0 = 64 * j + 4 * sub;
-        if (64 * j >= k) break;
-        if (c0 >= k) continue;   // k % 64 != 0: the last block is partial
-        float v[4];
-        if constexpr (TBF) {
-          const uint2 x = *reinterpret_cast<const uint2*>(
-              reinterpret_cast<const uint16_t*>(E) + id * k + c0);
-          v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
-          v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
-        } else {
-          const float4 x = *reinterpret_cast<const float4*>(
-              reinterpret_cast<const float*>(E) + id * k + c0);
-          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-        }
+        for (int j = 0; j < J; ++j) {
+          const int c0 = c00 + 64 * j + 4 * sub;
+          float v[4] = {0.f, 0.f, 0.f, 0.f};
+          if (live) {
+            if constexpr (TBF) {
+              const uint2 x = *reinterpret_cast<const uint2*>(
+                  reinterpret_cast<const uint16_t*>(E) + id * k + c0);
+              v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+              v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+            } else {
+              const float4 x = *reinterpret_cast<const float4*>(
+                  reinterpret_cast<const float*>(E) + id * k + c0);
+              v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+            }
+          }
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          s4[j][x] += v[x];
-          q4[j][x] += v[x] * v[x];
+          for (int x = 0; x < 4; ++x) {
+            s4[j][x] += v[x];
+            q4[j][x] += v[x] * v[x];
+          }
         }
       }
-    }
-    float y2 = 0.f;
+      if (live)
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
-      if (64 * j >= k) break;
-      if (64 * j + 4 * sub >= k) continue;
+        for (int j = 0; j < J; ++j)
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-        y2 += 0.5f * (s4[j][x] * s4[j][x] - q4[j][x]) * Wp[F + 64 * j + 4 * sub + x];
+          for (int x = 0; x < 4; ++x)
+            y2 += 0.5f * (s4[j][x] * s4[j][x] - q4[j][x]) * Wp[F + c00 + 64 * j + 4 * sub + x];
     }
     y2 = group_sum<16>(y2);
     if (sub == 0) {
@@ -1432,14 +1503,27 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
         const int64_t rows_per_block = 256 / 16;
         int64_t fb = (B + rows_per_block - 1) / rows_per_block;
         if (fb > 8192) fb = 8192;
-        if (tbf)
-          hipLaunchKernelGGL(dfm_fm_base<true>, dim3((unsigned)fb), dim3(256), 0, st, idx, B, F,
-                             E, M, k, w, Wp, bp, fm_base);
-        else
-          hipLaunchKernelGGL(dfm_fm_base<false>, dim3((unsigned)fb), dim3(256), 0, st, idx, B, F,
-                             E, M, k, w, Wp, bp, fm_base);
+#define HHFM_FMB(KJ)                                                                       \
+  if (tbf)                                                                                 \
+    hipLaunchKernelGGL((dfm_fm_base<true, KJ>), dim3((unsigned)fb), dim3(256), 0, st, idx, B, \
+                       F, E, M, k, w, Wp, bp, fm_base);                                    \
+  else                                                                                     \
+    hipLaunchKernelGGL((dfm_fm_base<false, KJ>), dim3((unsigned)fb), dim3(256), 0, st, idx,   \
+                       B, F, E, M, k, w, Wp, bp, fm_base);
+        switch (k % 64 ? 0 : k / 64) {
+          case 1: HHFM_FMB(1) break;
+          case 2: HHFM_FMB(2) break;
+          case 4: HHFM_FMB(4) break;
+          case 8: HHFM_FMB(8) break;
+          default: HHFM_FMB(0) break;
+        }
+#undef HHFM_FMB
       }
       a.fmbase = fm_base;
+      {
+        const char* e = getenv("HHFM_DFM_F32_STAGE");
+        a.stage = !(e && e[0] == '0');
+      }
       const int64_t units = (int64_t)(L - 1) * TM * 2 * 16 * TM * 4;
       const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
       hipLaunchKernelGGL(dfm_pack_weights_f32s, dim3(pblocks), dim3(256), 0, st, a, TM,

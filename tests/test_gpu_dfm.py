@@ -337,7 +337,8 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
     (dfm_fused_f32s) with the rows grouped by user (rows >= 64 x table rows):
     within the fp32 tolerance of the reference graph, equal to the ungrouped
     call up to summation order, and a row's score independent of its block
-    (a permuted batch gives the permuted scores bit for bit)."""
+    (a permuted batch gives the permuted scores bit for bit); P rows staged in
+    LDS or read from memory, 8- or 4-wave workgroups: the same bits."""
     from hhfm_amd import ops
     rng = np.random.default_rng(64)
     F, k, M, users, B = 5, 64, 997, 40, 70000
@@ -360,6 +361,16 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
     perm = rng.permutation(B)
     again = ops.dfm_forward(xd[torch.from_numpy(perm).cuda()], m.table, wb, Wt, bs, dims,
                             torch.float32, Wpd, bpd, proj=True).cpu().numpy()
+    monkeypatch.setenv("HHFM_DFM_F32_STAGE", "0")       # P rows from HBM/L2 only
+    unstaged = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                               proj=True).cpu().numpy()
+    assert np.array_equal(unstaged, got)                 # same values, same order
+    monkeypatch.setenv("HHFM_DFM_F32_WAVES", "4")        # 64-row workgroups
+    w4 = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                         proj=True).cpu().numpy()
+    assert np.array_equal(w4, got)
+    monkeypatch.delenv("HHFM_DFM_F32_WAVES")
+    monkeypatch.delenv("HHFM_DFM_F32_STAGE")
     monkeypatch.setenv("HHFM_DFM_F32_GROUP", "0")
     flat = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                            proj=True).cpu().numpy()
