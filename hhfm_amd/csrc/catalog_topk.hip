@@ -252,8 +252,9 @@ __global__ __launch_bounds__(256) void catalog_main(
                  : __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
   };
   auto tile_step = [&](const int tile, uint4 (&ar)[KT], float& wr) {
-    // global threshold hint: load now, consume after the MFMA chain
-    const int32_t gk = (q < B) ? gthr[q] : 0;
+    // global threshold hint: load now, consume after the MFMA chain (STORE:
+    // no selection, and the small-catalog path leaves gthr unset)
+    const int32_t gk = (!STORE && q < B) ? gthr[q] : 0;
     f32x16 acc = {0};
     const int nxt = tile + PF < tb1 ? tile + PF : tile;
     float wcur = wr;
@@ -1310,9 +1311,6 @@ extern "C" int hhfm_catalog_topk_ex(
   float* cst = reinterpret_cast<float*>(ws + p.off_cst);
   int32_t* gthr = reinterpret_cast<int32_t*>(ws + p.off_thr);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // 0x80808080 decodes to ~-3.4e38: below every finite score
-  const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
-  if (me != hipSuccess) return (int)me;
   const char* Eb = reinterpret_cast<const char*>(E);
   {
     const int rc = launch_check_query_ids(qidx, B, ncols, user_col, ctx_begin, ctx_end,
@@ -1396,6 +1394,12 @@ extern "C" int hhfm_catalog_topk_ex(
     return (int)hipGetLastError();
   }
 
+  {   // streaming path only: the per-query threshold hints start below every
+    // score (0x80808080 decodes to ~-3.4e38); the small-catalog paths never
+    // read them
+    const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
+    if (me != hipSuccess) return (int)me;
+  }
   // (bf16 k = 256 would spill at two waves per SIMD: catalog_main keeps it)
   const bool ring = K <= 32 && p.seed_n > 0 && (bf16 ? KT == 8 : (KT == 8 || KT == 16)) &&
                     !catalog_exact() && catalog_ring_on();
