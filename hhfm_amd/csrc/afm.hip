@@ -115,13 +115,16 @@ static size_t afm_rows_fused_lds(int k, int A, bool split) {
 // piece products of order >= 2^-16, 6 MFMAs per 16 k instead of 8
 // 32x32x2_f32 ones (512 -> 192 cycles).  A 16-k step's lane half h holds k
 // {16t+4h .. +3} and {16t+8+4h .. +3}: two of the exact kernel's 8-k steps.
-template <bool TBF, int NT, bool SPLIT>
+// KS > 0 (SPLIT only): k = 16·KS known at compile time, so the k loop unrolls
+// (no register rotation moves, constant gather offsets); KS = 0: any k.
+template <bool TBF, int NT, bool SPLIT, int KS = 0>
 __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_fused(
     const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
-    int k, const float* __restrict__ w, float w0, const float* __restrict__ Wt,
+    int k_arg, const float* __restrict__ w, float w0, const float* __restrict__ Wt,
     const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
     const float* __restrict__ P, float* __restrict__ out) {
   constexpr int NA = NT * 32;
+  const int k = KS > 0 ? 16 * KS : k_arg;
   extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_rows_fused_lds()
   float4* img = reinterpret_cast<float4*>(smem);
   uint4* imgb = reinterpret_cast<uint4*>(smem);   // SPLIT: 3 piece images [NA][k/8] x 16 B
@@ -228,7 +231,7 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
     // Σw of the row: lanes p < F of the row's group fetch one field each
     const float wf = (ok && p < F) ? w[clamp_id(idx[row * F + p], M)] : 0.f;
     if constexpr (SPLIT) {
-      for (int t2 = 0; t2 < KQ / 2; ++t2) {
+      auto step2 = [&](int t2) {
         // steps 2t2, 2t2+1 are in (xa, ya), (xb, yb); fetch the next pair
         float4 xn = xa, yn = ya, xm = xb, ym = yb;
         if (2 * t2 + 2 < KQ) {
@@ -267,6 +270,12 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
         ya = yn;
         xb = xm;
         yb = ym;
+      };
+      if constexpr (KS > 0) {
+#pragma unroll
+        for (int t2 = 0; t2 < KS; ++t2) step2(t2);
+      } else {
+        for (int t2 = 0; t2 < KQ / 2; ++t2) step2(t2);
       }
     } else
     for (int t = 0; t < KQ; ++t) {
@@ -759,12 +768,17 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       const bool split = k % 16 == 0 && !(ex && ex[0] == '1') &&
                          afm_rows_fused_lds(k, A, true) <= 160 * 1024;
       const size_t lds = afm_rows_fused_lds(k, A, split);
-#define HHFM_AFM_FUSED_L(N, TB, SP)                                                         \
+#define HHFM_AFM_FUSED_K(N, TB, SP, KS)                                                      \
   {                                                                                        \
-    allow_lds((const void*)afm_rows_fused<TB, N, SP>, lds);                                 \
-    hipLaunchKernelGGL((afm_rows_fused<TB, N, SP>), dim3((unsigned)blocks), dim3(256), lds, \
-                       st, idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, out); \
+    allow_lds((const void*)afm_rows_fused<TB, N, SP, KS>, lds);                             \
+    hipLaunchKernelGGL((afm_rows_fused<TB, N, SP, KS>), dim3((unsigned)blocks), dim3(256),  \
+                       lds, st, idx, B, F, E, features_M, k, w, w0, Wt, att_b, att_p, A, P, \
+                       out);                                                                \
   }
+#define HHFM_AFM_FUSED_L(N, TB, SP)                                                         \
+  if (SP && k == 64) HHFM_AFM_FUSED_K(N, TB, SP, 4)                                          \
+  else if (SP && k == 128) HHFM_AFM_FUSED_K(N, TB, SP, 8)                                    \
+  else HHFM_AFM_FUSED_K(N, TB, SP, 0)
 #define HHFM_AFM_FUSED(N)                                                                   \
   if (NT == N) {                                                                           \
     if (tb) {                                                                              \
@@ -780,6 +794,7 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       HHFM_AFM_FUSED(4)
 #undef HHFM_AFM_FUSED
 #undef HHFM_AFM_FUSED_L
+#undef HHFM_AFM_FUSED_K
     }
   }
   const int ntl = (A + GBN - 1) / GBN;
