@@ -383,3 +383,26 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
         err = np.abs(v - ref) / mag
         assert np.all(err <= 2e-5), (name, float(err.max()))
     assert np.array_equal(again, got[perm])
+
+
+@pytest.mark.parametrize("B,N", [(1, 4082), (300, 4082), (1024, 32768), (3000, 4082),
+                                 (77, 1100), (5000, 2048)])
+def test_topk_dense_split_waves(B, N, monkeypatch):
+    """Dense top-K with 4 or 2 waves per query (few queries, N >= 1,024: each
+    wave folds a 64-aligned slice, the first merges the lists) equals one wave
+    per query bit for bit and np.argsort's (score desc, index asc) order,
+    heavy ties included."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(B + N)
+    S = rng.integers(0, 200, size=(B, N)).astype(np.float32)   # many exact ties
+    S[:, ::7] += rng.normal(size=(B, (N + 6) // 7)).astype(np.float32)
+    Sd = torch.from_numpy(S).cuda()
+    for K in (1, 20, 64):
+        s, i = ops.topk_dense(Sd, K, 3)
+        monkeypatch.setenv("HHFM_TOPK_WPQ", "1")
+        s1, i1 = ops.topk_dense(Sd, K, 3)
+        monkeypatch.delenv("HHFM_TOPK_WPQ")
+        assert torch.equal(i, i1) and torch.equal(s, s1)
+        rs, ri = orc.top_k(S, K)
+        assert np.array_equal(i.cpu().numpy(), ri + 3)
+        assert np.array_equal(s.cpu().numpy(), rs)
