@@ -2,7 +2,7 @@
 """K2 at the C4 per-GPU shape (HHFM k=128, 1,024 queries x 1.25M-item shard,
 top-20): median kernel time per variant (HIP events), fp32 and bf16 tables.
 Variants are environment switches read per call (HHFM_CATALOG_SEED,
-HHFM_CATALOG_EXACT, HHFM_CATALOG_RING, HHFM_RING_QS via "qs2").  usage: python scripts/k2_c4.py [--reps N]"""
+HHFM_CATALOG_EXACT, HHFM_CATALOG_RING, HHFM_RING_PIPE=0 via "nopipe").  usage: python scripts/k2_c4.py [--reps N]"""
 import argparse
 import json
 import os
@@ -40,7 +40,7 @@ def main():
             os.environ["HHFM_CATALOG_SEED"] = "0" if "noseed" in var else "1"
             os.environ["HHFM_CATALOG_EXACT"] = "1" if "exact" in var else "0"
             os.environ["HHFM_CATALOG_RING"] = "0" if "noring" in var else "1"
-            os.environ["HHFM_RING_QS"] = "2" if "qs2" in var else "1"
+            os.environ["HHFM_RING_PIPE"] = "0" if "nopipe" in var else "1"
 
             def run():
                 return ops.catalog_topk(A, E, ops.MODE_HHFM, K, nu + 12, N, 0, None, 0,
