@@ -46,89 +46,14 @@
 // out[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c y2_c·Wp[F+c]) + bp) + Σ_n relu(h_L)·Wp[F+k+n]
 #include <hipcub/hipcub.hpp>
 
-#include "gemm_mfma.h"
+#include "dfm_fused.h"
 
 
 namespace hhfm {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
 bool dfm_f32_split();
 
-constexpr int kFusedMaxLayers = 4;
-constexpr int kFusedMaxF = 16;
-constexpr int kFusedMaxK = 512;
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
-constexpr int kLdsBytes = 160 * 1024;   // gfx950 LDS per workgroup
-constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
-
-struct FusedDfmArgs {
-  const int32_t* idx;
-  int64_t B;
-  int F, k;
-  const void* E;
-  int64_t M;
-  const float* w;
-  int L;
-  int dims[kFusedMaxLayers];
-  int ldb[kFusedMaxLayers];
-  const uint16_t* Wt[kFusedMaxLayers];
-  const float* bias[kFusedMaxLayers];
-  const float* Wp;
-  float bp;
-  float* out;
-  const uint4* packed;   // chunk sequence written by dfm_pack_weights
-  // PROJ: fp32 P_f[id] at proj + f·proj_fstride + id·proj_ld (f counted from
-  // the first projected field), zero beyond
-  // dims[0]; fp32 MLP: natural unit order; bf16 MLP: the accumulator order of
-  // dfm_proj_pos (a lane's 16 units of a tile are contiguous)
-  const void* proj;
-  int64_t proj_fstride;
-  int proj_ld;           // row stride: projected fields x 32·TM
-  int Fd;                // fields [0, Fd) run layer 0 on MFMA, [Fd, F) come from P
-                         // (Fd = F: no projection; 0: all fields projected)
-  // bf16 kernel: internal field j is the caller's field (perm >> 4j) & 15
-  // (direct fields first); row m's score goes to out[order[m]] when order is
-  // set (idx then holds the caller's rows regrouped, dfm_order_rows).  The
-  // fp32 kernel takes the identity and no order.
-  uint64_t perm;
-  const int32_t* order;
-  // dfm_fused_f32s: base[m] = (Σ_f w·Wp + FM part) + bp from dfm_fm_base;
-  // stage: P rows of narrow-span fields staged in LDS (HHFM_DFM_F32_STAGE=0: off)
-  const float* fmbase;
-  int stage;
-};
-
-HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
-  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
-  return __builtin_bit_cast(uint32_t, v);
-}
-
-// One lane-linear 16-B-per-lane LDS-DMA (global_load_lds_dwordx4, M0 = the
-// wave's LDS destination) issued through inline asm.  When the compiler sees
-// the DMA builtin it treats it as an LDS access of unknown order and drains
-// every ds_read with lgkmcnt(0) at each MFMA step boundary; issued this way
-// it keeps counted lgkmcnt waits (1 % on C5 ITEM/CTX, profiles/r02_k3_hidden_knockouts.txt).
-// The compiler does not track these loads: every barrier that publishes them
-// is preceded by an explicit s_waitcnt vmcnt(0) (dma_wait below).
-HHFM_DEV void lds_dma16(const void* gsrc, void* lds_dst) {
-  const uint32_t m0v = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_dst);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(gsrc), "s"(m0v)
-               : "memory");
-}
-
-HHFM_DEV void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-HHFM_DEV void swap_halves(uint32_t& a, uint32_t& b) {
-  // lanes 32-63 of a <-> lanes 0-31 of b
-  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
-  a = r[0];
-  b = r[1];
-}
 
 // Chunk g, row n, slot u' holds 8 bf16 of source unit u = u' ^ ((n>>1)&7):
 //   layer 0, chunk c:  step S = 4c + u/2 -> W0[n][(S%F)·k + 16(S/F) + 8(u&1) ..]
@@ -163,10 +88,6 @@ __global__ __launch_bounds__(256) void dfm_pack_weights(FusedDfmArgs a, int TM, 
   }
 }
 
-template <bool B>
-struct BoolC {
-  static constexpr bool value = B;
-};
 
 template <bool TBF, int TM, bool PROJ>
 __global__ __launch_bounds__(256, 1) void dfm_fused(FusedDfmArgs a) {
@@ -1461,6 +1382,12 @@ static int dfm_f32_waves() {
 }
 
 
+// HHFM_DFM_WIDE=0: the ITEM plan keeps the 128-row kernel (dfm_fused)
+static bool dfm_wide_enabled() {
+  const char* e = getenv("HHFM_DFM_WIDE");
+  return !(e && e[0] == '0');
+}
+
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
@@ -1582,6 +1509,9 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
 #undef HHFM_FUSED32
     return true;
   }
+  // the ITEM plan at an instantiated shape: 256 rows per workgroup (dfm_wide.hip)
+  if (pj && tbf && a.Fd == 1 && L == 3 && dfm_wide_enabled() && dfm_wide_launch(a, TM, st))
+    return true;
   const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
   const int nS = a.Fd * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;
   const int64_t units = (int64_t)(nc0 + (L - 1) * NC) * 32 * TM * 8;

@@ -1,0 +1,467 @@
+// K3w — DeepFM forward, bf16 MLP, ITEM plan, 256 rows per workgroup.
+// Replaces DeepFM.out (Newcode/DFM.py:104-137) like dfm_fused.hip's kernels;
+// planned by hhfm_dfm_forward_workspace_ex / hhfm_dfm_catalog_topk
+// (mlp_gemm.hip) through dfm_fused_launch.
+#include <utility>
+
+#include "dfm_fused.h"
+
+namespace hhfm {
+
+// ---------------------------------------------------------------------------
+// K3w — the bf16-MLP DeepFM forward at 192 rows per workgroup (the ITEM plan:
+// layer 0 of the item field on MFMA, every other field from P, rows grouped
+// by user).  dfm_fused keeps 32 rows x all output units per wave in
+// accumulators (208 registers), so its workgroup holds 128 rows and streams
+// every weight once per 128 rows: ≈32 B/clk of L2 -> LDS per CU at the MFMA
+// rate, what one CU pulls — the C5 kernel ran at that stream, MFMA busy 35 %.
+// Here a wave owns 48 rows (three 16-row tiles, v_mfma_f32_16x16x32_bf16) and
+// walks the output units 32 at a time: per pass, the full-K MFMA chain of
+// 2 unit tiles x 3 row tiles (24 accumulator registers), then bias + ReLU +
+// bf16 straight into the next layer's B operand — the 16x16 result puts
+// units 4kq..+3 of a tile on lane group kq, exactly the k a lane group
+// supplies next (k order {32s + 4kq .. +3, 32s + 16 + 4kq .. +3}), so no
+// lane movement.  Live: the layer input (156 registers for 48 rows x 416
+// units) + the output being built (156) + 24, at one wave per SIMD; the
+// weight stream per row falls to 2/3 (≈21 B/clk per CU), each 1-KB A
+// fragment feeds three MFMAs.
+//   * weights: dfm_pack_weights_w lays each (layer, 32-unit pass) out as S
+//     k32 steps of 2 KB, [unit tile j][kq][unit r] x 16 B (lane-linear, no
+//     bank conflicts); a 3-slot LDS ring filled two passes ahead by
+//     lane-linear LDS-DMA, one counted vmcnt + barrier per pass, the DMAs
+//     issued one per MFMA step;
+//   * layer 0 = Σ_f P_f[x_f] (projected fields, staged in LDS when the
+//     block's id spans fit) + the item field's k32 steps on MFMA, B = the
+//     gathered item rows (k order 32s + 8kq .. +7);
+//   * the FM part from the item's B operand registers and the other fields'
+//     table rows, before layer 0.
+// Instantiated per shape (TM 32-unit passes in every layer, S0 = k/32 item
+// steps, NF projected fields); other shapes take dfm_fused.
+// ---------------------------------------------------------------------------
+constexpr int kWideRows = 192;
+
+template <int B_, int E_, class Fn>
+HHFM_DEV void static_for(Fn&& fn) {
+  if constexpr (B_ < E_) {
+    fn(std::integral_constant<int, B_>{});
+    static_for<B_ + 1, E_>(fn);
+  }
+}
+
+// the wave's DMAs older than its N most recent have landed, every wave's LDS
+// reads have returned, then the block barrier
+template <int N>
+HHFM_DEV void vm_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// materialise a value here: the compiler sinks pure arithmetic towards its
+// last use (the store after the last layer), keeping its inputs live
+HHFM_DEV void pin(float& v) { asm volatile("" : "+v"(v)); }
+HHFM_DEV void pin(uint4& v) {
+  u32x4_t t = __builtin_bit_cast(u32x4_t, v);
+  asm volatile("" : "+v"(t));
+  v = __builtin_bit_cast(uint4, t);
+}
+
+// one lane-linear 16-B-per-lane LDS-DMA to the LDS byte offset lds_off
+HHFM_DEV void dma16_at(const void* gsrc, uint32_t lds_off) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_off))
+               : "memory");
+}
+
+// pass (layer i, t), k32 step s, unit tile j, lane (r, kq): 16 B of
+//   layer 0: W0[32t + 16j + r][fe0·k + 32s + 8kq .. +7]
+//   layer i: W_i[32t + 16j + r][32s + 4kq .. +3] ++ W_i[..][32s + 16 + 4kq .. +3]
+// zero outside the layer's rows / columns
+__global__ __launch_bounds__(256) void dfm_pack_weights_w(FusedDfmArgs a, int TM, int S0,
+                                                          uint4* __restrict__ out) {
+  const int64_t n0 = (int64_t)TM * S0 * 2;            // layer-0 1-KB units
+  const int64_t total = (n0 + 2 * (int64_t)TM * TM * 2) * 64;
+  const int fe0 = (int)(a.perm & 15);   // caller field of internal field 0 (the item)
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t unit = x >> 6;
+    const int lane = (int)(x & 63), r = lane & 15, kq = lane >> 4;
+    int i, t, sj;
+    if (unit < n0) {
+      i = 0;
+      t = (int)(unit / (2 * S0));
+      sj = (int)(unit % (2 * S0));
+    } else {
+      const int64_t rel = unit - n0;
+      i = 1 + (int)(rel / (2 * (int64_t)TM * TM));
+      const int rr = (int)(rel % (2 * (int64_t)TM * TM));
+      t = rr / (2 * TM);
+      sj = rr % (2 * TM);
+    }
+    const int s = sj >> 1, j = sj & 1;
+    const int n = 32 * t + 16 * j + r;
+    const uint16_t* row = a.Wt[i] + (int64_t)n * a.ldb[i];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < a.dims[i]) {
+      if (i == 0) {
+        v = *reinterpret_cast<const uint4*>(row + fe0 * a.k + 32 * s + 8 * kq);
+      } else {
+        const int c0 = 32 * s + 4 * kq, c1 = c0 + 16;
+        if (c0 < a.ldb[i]) {
+          const uint2 lo = *reinterpret_cast<const uint2*>(row + c0);
+          v.x = lo.x;
+          v.y = lo.y;
+        }
+        if (c1 < a.ldb[i]) {
+          const uint2 hi = *reinterpret_cast<const uint2*>(row + c1);
+          v.z = hi.x;
+          v.w = hi.y;
+        }
+      }
+    }
+    out[x] = v;
+  }
+}
+
+template <int TM, int S0, int NF>
+__global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
+  static_assert(NF >= 1 && NF < kFusedMaxF, "wide DeepFM kernel: fields");
+  constexpr int F = NF + 1;
+  constexpr int NR = TM * 32;
+  constexpr int NCH = 3 * TM;                          // passes: (layer, 32 units)
+  constexpr int kUnits = 2 * (TM > S0 ? TM : S0);      // 1-KB units per ring slot
+  constexpr int kSlotB = kUnits * 1024;
+  constexpr int kIds = 3 * kSlotB;
+  constexpr int kBl = kIds + kWideRows * kFusedMaxF * 4;
+  constexpr int kVl = kBl + 3 * NR * 4;
+  constexpr int kWp = kVl + NR * 4;
+  constexpr int kPlo = kWp + (kFusedMaxF + kFusedMaxK) * 4;
+  constexpr int kYl = kPlo + 4 * kFusedMaxF * 4;
+  constexpr int kPst = kYl + kWideRows * 4;
+  constexpr int kPsLd = NR + 4;                        // staged P row stride (floats)
+  constexpr int kPsFloats = (kLdsBytes - kPst) / 4;
+  static_assert(kPst + 4 * 1024 <= kLdsBytes, "wide DeepFM kernel: LDS");
+  __shared__ __attribute__((aligned(16))) char smem[kLdsBytes];   // ONE LDS object
+  int32_t* ids = reinterpret_cast<int32_t*>(smem + kIds);
+  float* blv = reinterpret_cast<float*>(smem + kBl);
+  float* vl = reinterpret_cast<float*>(smem + kVl);
+  float* wpl = reinterpret_cast<float*>(smem + kWp);
+  int32_t* plo = reinterpret_cast<int32_t*>(smem + kPlo);   // lo | hi | P base | E base
+  float* ylds = reinterpret_cast<float*>(smem + kYl);
+  float* pst = reinterpret_cast<float*>(smem + kPst);
+
+  const int tid = threadIdx.x, l = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = l & 15, kq = l >> 4;
+  const int64_t m0 = (int64_t)blockIdx.x * kWideRows;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const int k = a.k;
+  const float* P = reinterpret_cast<const float*>(a.proj);
+  const uint16_t* E = reinterpret_cast<const uint16_t*>(a.E);
+
+  // rows past B repeat row B-1 (never stored), so the id spans stay tight
+  for (int x = tid; x < kWideRows * F; x += 256) {
+    int64_t m = m0 + x / F;
+    m = m < a.B ? m : a.B - 1;
+    const int fe = (int)((a.perm >> (4 * (x % F))) & 15);
+    ids[x] = clamp_id(a.idx[m * F + fe], a.M);
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[2] ? a.Wp[F + k + n] : 0.f;
+  for (int x = tid; x < F + k; x += 256)
+    wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x < F ? (int)((a.perm >> (4 * x)) & 15) : x];
+  if (tid < kFusedMaxF) {
+    plo[tid] = 0x7fffffff;
+    plo[kFusedMaxF + tid] = -1;
+  }
+  __syncthreads();
+
+  // pass c: 2·S k32-step halves of 1 KB at unit cbase(c) -> ring slot c % 3
+  auto cunits = [](int c) { return c < TM ? 2 * S0 : 2 * TM; };
+  auto cbase = [](int c) { return c < TM ? c * 2 * S0 : TM * 2 * S0 + (c - TM) * 2 * TM; };
+  auto dma_unit = [&](int c, int u) {
+    dma16_at(a.packed + (int64_t)(cbase(c) + u) * 64 + l, lds0 + (c % 3) * kSlotB + u * 1024);
+  };
+  for (int c = 0; c < 2; ++c)
+    for (int u = wv; u < cunits(c); u += 4) dma_unit(c, u);
+
+  // layer 0's B operand: the item rows of this lane's three rows (k32 step
+  // s: columns 32s + 8kq .. +7), in flight with the weight passes
+  const int row0 = 48 * wv + r;            // row tile rt: row0 + 16·rt
+  uint4 E0[3][S0];
+#pragma unroll
+  for (int rt = 0; rt < 3; ++rt) {
+    const int64_t id = ids[(row0 + 16 * rt) * F];
+#pragma unroll
+    for (int s = 0; s < S0; ++s)
+      E0[rt][s] = *reinterpret_cast<const uint4*>(E + id * k + 32 * s + 8 * kq);
+  }
+  if (tid < kWideRows) {   // Σ_f w[x_f]·Wp[f], one row per thread (dfm_fused's order)
+    float wv8[kFusedMaxF];
+#pragma unroll
+    for (int f = 0; f < kFusedMaxF; ++f) wv8[f] = f < F ? a.w[ids[tid * F + f]] : 0.f;
+    float y1 = 0.f;
+#pragma unroll
+    for (int f = 0; f < kFusedMaxF; ++f)
+      if (f < F) y1 += wv8[f] * wpl[f];
+    ylds[tid] = y1;
+  }
+  for (int x = tid; x < kWideRows * NF; x += 256) {
+    const int row = x / NF, f = 1 + x % NF;
+    atomicMin(&plo[f], ids[row * F + f]);
+    atomicMax(&plo[kFusedMaxF + f], ids[row * F + f]);
+  }
+  __syncthreads();
+  // all projected fields' P rows and table rows lo..hi staged in LDS when
+  // they fit (rows grouped by user: the user's and the contexts' few rows);
+  // otherwise the block reads them from memory.  The body is compiled once
+  // per case: a uniform branch per field between LDS and memory reads is
+  // merged by the compiler into flat loads.
+  const int ek = k / 2;   // bf16 table row in floats
+  bool allfit;
+  {
+    int used = 0;
+    for (int f = 1; f < F; ++f) {
+      const int span = plo[kFusedMaxF + f] - plo[f] + 1;
+      if (tid == 0) {
+        plo[2 * kFusedMaxF + f] = used;
+        plo[3 * kFusedMaxF + f] = used + span * kPsLd;
+      }
+      used += span * (kPsLd + ek);
+    }
+    allfit = used <= kPsFloats;
+  }
+  if (allfit) {
+    int used = 0;
+    for (int f = 1; f < F; ++f) {
+      const int lo = plo[f], span = plo[kFusedMaxF + f] - lo + 1;
+      for (int x = tid; x < span * (NR / 4); x += 256) {
+        const int row = x / (NR / 4), c4 = x % (NR / 4);
+        *reinterpret_cast<float4*>(pst + used + row * kPsLd + 4 * c4) =
+            *reinterpret_cast<const float4*>(P + (f - 1) * a.proj_fstride +
+                                             (int64_t)(lo + row) * a.proj_ld + 4 * c4);
+      }
+      const float4* Ef = reinterpret_cast<const float4*>(
+          reinterpret_cast<const float*>(a.E) + (int64_t)lo * ek);
+      float4* dst = reinterpret_cast<float4*>(pst + used + span * kPsLd);
+      for (int x = tid; x < span * ek / 4; x += 256) dst[x] = Ef[x];
+      used += span * (kPsLd + ek);
+    }
+  }
+  dma_wait();
+  __syncthreads();   // passes 0 and 1, the item rows, the staged rows, the plan
+
+  auto body = [&](auto stc) {
+    constexpr bool ST = decltype(stc)::value;
+    // layer inputs in B-operand form, one uint4 per (row tile, k32 step)
+    uint4 X[3][TM], Y[3][TM];
+    float y2[3] = {0.f, 0.f, 0.f}, part[3] = {0.f, 0.f, 0.f};
+    int pid[3][F];   // this lane's rows' ids (projected fields)
+#pragma unroll
+    for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+      for (int f = 1; f < F; ++f) pid[rt][f] = ids[(row0 + 16 * rt) * F + f];
+
+    // FM second-order part (DFM.py:114-122) before layer 0: per k32 step,
+    // the item's 8 columns 32s + 8kq .. +7 from its B operand, the other
+    // fields' from their rows; lane groups summed at the end
+#pragma unroll
+    for (int s = 0; s < S0; ++s) {
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt) {
+        const uint4 ex = E0[rt][s];
+        const uint32_t x4[4] = {ex.x, ex.y, ex.z, ex.w};
+        float fs[8], fq[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v0 = __uint_as_float(x4[q] << 16), v1 = __uint_as_float(x4[q] & 0xffff0000u);
+          fs[2 * q] = v0;
+          fq[2 * q] = v0 * v0;
+          fs[2 * q + 1] = v1;
+          fq[2 * q + 1] = v1 * v1;
+        }
+#pragma unroll
+        for (int f2 = 1; f2 < F; ++f2) {
+          uint4 u;
+          if constexpr (ST)
+            u = *reinterpret_cast<const uint4*>(
+                reinterpret_cast<const uint16_t*>(pst + plo[3 * kFusedMaxF + f2]) +
+                (pid[rt][f2] - plo[f2]) * k + 32 * s + 8 * kq);
+          else
+            u = *reinterpret_cast<const uint4*>(E + (int64_t)pid[rt][f2] * k + 32 * s + 8 * kq);
+          const uint32_t u4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float u0 = __uint_as_float(u4[q] << 16), u1 = __uint_as_float(u4[q] & 0xffff0000u);
+            fs[2 * q] += u0;
+            fq[2 * q] += u0 * u0;
+            fs[2 * q + 1] += u1;
+            fq[2 * q + 1] += u1 * u1;
+          }
+        }
+        const float4* wc = reinterpret_cast<const float4*>(wpl + kFusedMaxF + 32 * s + 8 * kq);
+        const float4 w0 = wc[0], w1 = wc[1];
+        const float wq[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        float d = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) d += 0.5f * (fs[q] * fs[q] - fq[q]) * wq[q];
+        y2[rt] += d;
+        // one step at a time: the fence keeps the loads of later steps below,
+        // the pin keeps this step's arithmetic here (otherwise the compiler
+        // sinks it to the store at the end and keeps every loaded row live)
+        pin(y2[rt]);
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    // P_f rows of this lane's three rows, units 32t + 16j + 4kq .. +3 (at
+    // dfm_proj_pos of the first: 4 contiguous floats), summed into acc
+    auto psum = [&](int t, f32x4 (&acc)[3][2]) {
+      const int pos0 = 32 * t + 16 * (kq & 1) + 4 * (kq >> 1);   // j = 0; j = 1: +8
+#pragma unroll
+      for (int f = 1; f < F; ++f) {
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          const float* pp;
+          if constexpr (ST)
+            pp = pst + plo[2 * kFusedMaxF + f] + (pid[rt][f] - plo[f]) * kPsLd + pos0;
+          else
+            pp = P + (f - 1) * a.proj_fstride + (int64_t)pid[rt][f] * a.proj_ld + pos0;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const float4 x = *reinterpret_cast<const float4*>(pp + 8 * j);
+            acc[rt][j][0] += x.x;
+            acc[rt][j][1] += x.y;
+            acc[rt][j][2] += x.z;
+            acc[rt][j][3] += x.w;
+          }
+        }
+      }
+    };
+
+    static_for<0, NCH>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      constexpr int layer = p / TM, t = p % TM;
+      constexpr int S = layer == 0 ? S0 : TM;
+      constexpr int Unext = p + 1 < NCH ? (p + 1 < TM ? 2 * S0 : 2 * TM) : 0;
+      if constexpr (p > 0) vm_barrier<Unext / 4>();   // pass p landed; slot (p+2)%3 free
+      const uint4* wsl = reinterpret_cast<const uint4*>(smem + (p % 3) * kSlotB) + l;
+      // this wave's DMAs of pass p+2: units wv, wv+4, ..., one per MFMA step
+      const int Udma = p + 2 < NCH ? cunits(p + 2) : 0;
+      int dq = wv;
+      f32x4 acc[3][2];
+#pragma unroll
+      for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (layer == 0) psum(t, acc);
+      uint4 fa0 = wsl[0], fa1 = wsl[64];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        const bf16x8 a0 = __builtin_bit_cast(bf16x8, fa0), a1 = __builtin_bit_cast(bf16x8, fa1);
+        if (s + 1 < S) {
+          fa0 = wsl[128 * (s + 1)];
+          fa1 = wsl[128 * (s + 1) + 64];
+        }
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          uint4 bx;
+          if constexpr (layer == 0)
+            bx = E0[rt][s];
+          else if constexpr (layer == 1)
+            bx = X[rt][s];
+          else
+            bx = Y[rt][s];
+          const bf16x8 b = __builtin_bit_cast(bf16x8, bx);
+          acc[rt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, acc[rt][0], 0, 0, 0);
+          acc[rt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, acc[rt][1], 0, 0, 0);
+        }
+        if (dq < Udma) {
+          dma_unit(p + 2, dq);
+          dq += 4;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the next fragment reads behind this step
+      }
+      while (dq < Udma) {
+        dma_unit(p + 2, dq);
+        dq += 4;
+      }
+      const float* bl = blv + layer * NR + 32 * t + 4 * kq;
+      const float4 b0 = *reinterpret_cast<const float4*>(bl);
+      const float4 b1 = *reinterpret_cast<const float4*>(bl + 16);
+      if constexpr (layer < 2) {
+        // bias + ReLU (DFM.py:127-128) + bf16: units 32t + 4kq .. +3 and
+        // 32t + 16 + 4kq .. +3 are lane group kq's k of step t next layer
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
+          const uint4 o = make_uint4(
+              pack_bf16x2(fmaxf(c0[0] + b0.x, 0.f), fmaxf(c0[1] + b0.y, 0.f)),
+              pack_bf16x2(fmaxf(c0[2] + b0.z, 0.f), fmaxf(c0[3] + b0.w, 0.f)),
+              pack_bf16x2(fmaxf(c1[0] + b1.x, 0.f), fmaxf(c1[1] + b1.y, 0.f)),
+              pack_bf16x2(fmaxf(c1[2] + b1.z, 0.f), fmaxf(c1[3] + b1.w, 0.f)));
+          if constexpr (layer == 0)
+            X[rt][t] = o;
+          else
+            Y[rt][t] = o;
+          pin(layer == 0 ? X[rt][t] : Y[rt][t]);
+        }
+      } else {
+        const float* vv = vl + 32 * t + 4 * kq;
+        const float4 v0 = *reinterpret_cast<const float4*>(vv);
+        const float4 v1 = *reinterpret_cast<const float4*>(vv + 16);
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
+          part[rt] += fmaxf(c0[0] + b0.x, 0.f) * v0.x;
+          part[rt] += fmaxf(c0[1] + b0.y, 0.f) * v0.y;
+          part[rt] += fmaxf(c0[2] + b0.z, 0.f) * v0.z;
+          part[rt] += fmaxf(c0[3] + b0.w, 0.f) * v0.w;
+          part[rt] += fmaxf(c1[0] + b1.x, 0.f) * v1.x;
+          part[rt] += fmaxf(c1[1] + b1.y, 0.f) * v1.y;
+          part[rt] += fmaxf(c1[2] + b1.z, 0.f) * v1.z;
+          part[rt] += fmaxf(c1[3] + b1.w, 0.f) * v1.w;
+          pin(part[rt]);
+        }
+      }
+    });
+
+#pragma unroll
+    for (int rt = 0; rt < 3; ++rt) {
+      float pt = part[rt], yy = y2[rt];
+      pt += __shfl_xor(pt, 16, kWave);
+      pt += __shfl_xor(pt, 32, kWave);
+      yy += __shfl_xor(yy, 16, kWave);
+      yy += __shfl_xor(yy, 32, kWave);
+      const int row = row0 + 16 * rt;
+      const int64_t m = m0 + row;
+      if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
+    }
+  };
+  if (allfit) body(BoolC<true>{});
+  else body(BoolC<false>{});
+}
+
+bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st) {
+  bool ok = a.L == 3 && a.Fd == 1 && a.k % 32 == 0;
+  for (int i = 0; i < 3; ++i) ok = ok && (a.dims[i] + 31) / 32 == TM;
+  if (!ok) return false;
+  const int S0 = a.k / 32;
+  const dim3 grid((unsigned)((a.B + kWideRows - 1) / kWideRows));
+  const int64_t units = ((int64_t)TM * S0 * 2 + 2 * (int64_t)TM * TM * 2) * 64;
+  const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+  uint4* packed = const_cast<uint4*>(a.packed);
+#define HHFM_WIDE(T, A, N)                                                                 \
+  if (TM == T && S0 == A && a.F == N + 1) {                                                \
+    hipLaunchKernelGGL(dfm_pack_weights_w, dim3(pblocks), dim3(256), 0, st, a, T, A, packed); \
+    hipLaunchKernelGGL((dfm_fused_w<T, A, N>), grid, dim3(256), 0, st, a);                 \
+    return true;                                                                           \
+  }
+  HHFM_WIDE(13, 8, 4)   // C5: F = 5, k = 256, 3 x 400
+  HHFM_WIDE(5, 2, 4)    // tests: F = 5, k = 64, 3 x 150
+#undef HHFM_WIDE
+  return false;
+}
+
+}  // namespace hhfm

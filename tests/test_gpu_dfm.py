@@ -406,3 +406,51 @@ def test_topk_dense_split_waves(B, N, monkeypatch):
         rs, ri = orc.top_k(S, K)
         assert np.array_equal(i.cpu().numpy(), ri + 3)
         assert np.array_equal(s.cpu().numpy(), rs)
+
+
+@pytest.mark.parametrize("k,layers,B,grouped", [(256, [400, 400, 400], 50000, True),
+                                                (256, [400, 400, 400], 3000, False),
+                                                (64, [150, 150, 150], 20000, True),
+                                                (64, [150, 150, 150], 777, False)])
+def test_dfm_wide_item(k, layers, B, grouped, monkeypatch):
+    """The 192-row ITEM kernel (dfm_wide.hip, shapes it is instantiated for:
+    F = 5 with k = 256 / 3 x 400 — C5 — and k = 64 / 3 x 150): against the
+    bf16-rounding oracle (5e-3 of the magnitude) and the 128-row kernel
+    (HHFM_DFM_WIDE=0), with rows grouped by user (blocks stage their P and
+    table rows in LDS) and with random ids (blocks read them from memory,
+    B not a multiple of 192); a row's score never depends on its block."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(k + B)
+    nu, ni, ctx = 957, 4082, (7, 2, 3)
+    M = nu + ni + sum(ctx)
+    m = _model((nu, ni, M, 5, k, layers), mlp_dtype=torch.bfloat16,
+               table_dtype=torch.bfloat16)
+    cols = [rng.integers(0, nu if grouped else M, B), rng.integers(nu, nu + ni, B)]
+    off = nu + ni
+    for c in ctx:
+        cols.append(rng.integers(off, off + c, B) if grouped else rng.integers(0, M, B))
+        off += c
+    X = np.stack(cols, 1).astype(np.int32)
+    W = m.get_weights()
+    Ls = [W[f"layer_{i}"] for i in range(3)]
+    Bs = [W[f"bias_{i}"] for i in range(3)]
+    E, w = bf16_round(W["feature_embeddings"]), W["feature_bias"][:, 0]
+    Wp, bp = W["concat_projection"], float(W["concat_bias"])
+    Wt, bs, dims, Wpd, bpd = m._prepared()
+    wb = m.weights["feature_bias"].reshape(-1)
+    xd = torch.from_numpy(X).cuda()
+
+    def run(x, wide):
+        monkeypatch.setenv("HHFM_DFM_WIDE", "1" if wide else "0")
+        return ops.dfm_forward(x, m.table, wb, Wt, bs, dims, torch.bfloat16, Wpd, bpd,
+                               proj="item").cpu().numpy()
+
+    got = run(xd, True)
+    old = run(xd, False)
+    perm = rng.permutation(B)
+    again = run(xd[torch.from_numpy(perm).cuda()], True)
+    mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
+    ref = _bf16_oracle(X, E, w, Ls, Bs, Wp, bp)
+    assert np.all(np.abs(got - ref) <= 5e-3 * mag), np.max(np.abs(got - ref) / mag)
+    assert np.all(np.abs(got - old) <= 5e-3 * mag), np.max(np.abs(got - old) / mag)
+    assert np.array_equal(again, got[perm])
