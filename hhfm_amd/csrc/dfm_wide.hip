@@ -40,6 +40,13 @@ namespace hhfm {
 // ---------------------------------------------------------------------------
 constexpr int kWideRows = 192;
 
+// diagnostic knock-outs (timing only, wrong results; default 0): 1 FM part,
+// 2 P sums, 4 per-pass barriers, 8 weight DMA after the first two passes,
+// 16 MFMAs, 32 staging copies
+#ifndef HHFM_WKO
+#define HHFM_WKO 0
+#endif
+
 template <int B_, int E_, class Fn>
 HHFM_DEV void static_for(Fn&& fn) {
   if constexpr (B_ < E_) {
@@ -231,7 +238,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     }
     allfit = used <= kPsFloats;
   }
-  if (allfit) {
+  if (allfit && !(HHFM_WKO & 32)) {
     int used = 0;
     for (int f = 1; f < F; ++f) {
       const int lo = plo[f], span = plo[kFusedMaxF + f] - lo + 1;
@@ -266,7 +273,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     // the item's 8 columns 32s + 8kq .. +7 from its B operand, the other
     // fields' from their rows; lane groups summed at the end
 #pragma unroll
-    for (int s = 0; s < S0; ++s) {
+    for (int s = 0; s < ((HHFM_WKO & 1) ? 0 : S0); ++s) {
 #pragma unroll
       for (int rt = 0; rt < 3; ++rt) {
         const uint4 ex = E0[rt][s];
@@ -345,17 +352,17 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       constexpr int layer = p / TM, t = p % TM;
       constexpr int S = layer == 0 ? S0 : TM;
       constexpr int Unext = p + 1 < NCH ? (p + 1 < TM ? 2 * S0 : 2 * TM) : 0;
-      if constexpr (p > 0) vm_barrier<Unext / 4>();   // pass p landed; slot (p+2)%3 free
+      if constexpr (p > 0 && !(HHFM_WKO & 4)) vm_barrier<Unext / 4>();   // pass p landed; slot (p+2)%3 free
       const uint4* wsl = reinterpret_cast<const uint4*>(smem + (p % 3) * kSlotB) + l;
       // this wave's DMAs of pass p+2: units wv, wv+4, ..., one per MFMA step
-      const int Udma = p + 2 < NCH ? cunits(p + 2) : 0;
+      const int Udma = p + 2 < NCH && !(HHFM_WKO & 8) ? cunits(p + 2) : 0;
       int dq = wv;
       f32x4 acc[3][2];
 #pragma unroll
       for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (layer == 0) psum(t, acc);
+      if constexpr (layer == 0 && !(HHFM_WKO & 2)) psum(t, acc);
       uint4 fa0 = wsl[0], fa1 = wsl[64];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -374,8 +381,13 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
           else
             bx = Y[rt][s];
           const bf16x8 b = __builtin_bit_cast(bf16x8, bx);
+#if HHFM_WKO & 16
+          acc[rt][0][0] += (float)b[0] * (float)a0[0];
+          acc[rt][1][0] += (float)b[1] * (float)a1[0];
+#else
           acc[rt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b, acc[rt][0], 0, 0, 0);
           acc[rt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, acc[rt][1], 0, 0, 0);
+#endif
         }
         if (dq < Udma) {
           dma_unit(p + 2, dq);

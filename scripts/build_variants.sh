@@ -9,10 +9,10 @@ make -s native
 others=$(ls build/*.o | grep -v "build/$src.o")
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
-  mkdir -p ab/$name
+  mkdir -p ${AB_DIR:-ab}/$name
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
     $defs -c hhfm_amd/csrc/$src.hip -o build/var_$name.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab/$name/libhhfm.so $others build/var_$name.o
-  cp hhfm_amd/lib/_hhfm*.so ab/$name/
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ${AB_DIR:-ab}/$name/libhhfm.so $others build/var_$name.o
+  cp hhfm_amd/lib/_hhfm*.so ${AB_DIR:-ab}/$name/
   rm build/var_$name.o
 done
