@@ -46,6 +46,16 @@ constexpr int kWideRows = 192;
 #ifndef HHFM_WKO
 #define HHFM_WKO 0
 #endif
+// FM part of staged blocks: the fields' Σ_k Wp_k·e_k² from per-row sums g
+// computed once per staged table row (0: per row and k, as unstaged blocks)
+#ifndef HHFM_WFM
+#define HHFM_WFM 1
+#endif
+// staged blocks: P sums of layer-0 pass t+1 among pass t's MFMA steps (0: at
+// the pass start)
+#ifndef HHFM_WPI
+#define HHFM_WPI 1
+#endif
 
 template <int B_, int E_, class Fn>
 HHFM_DEV void static_for(Fn&& fn) {
@@ -69,6 +79,14 @@ HHFM_DEV void pin(uint4& v) {
   u32x4_t t = __builtin_bit_cast(u32x4_t, v);
   asm volatile("" : "+v"(t));
   v = __builtin_bit_cast(uint4, t);
+}
+
+// ReLU of two packed bf16 values: v_pk_max_i16 against 0
+// (asm: the compiler otherwise splits the pair and converts each half alone)
+HHFM_DEV uint32_t relu_bf16x2(uint32_t v) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(v));
+  return r;
 }
 
 // one lane-linear 16-B-per-lane LDS-DMA to the LDS byte offset lds_off
@@ -142,7 +160,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   constexpr int kVl = kBl + 3 * NR * 4;
   constexpr int kWp = kVl + NR * 4;
   constexpr int kPlo = kWp + (kFusedMaxF + kFusedMaxK) * 4;
-  constexpr int kYl = kPlo + 4 * kFusedMaxF * 4;
+  constexpr int kYl = kPlo + 5 * kFusedMaxF * 4;
   constexpr int kPst = kYl + kWideRows * 4;
   constexpr int kPsLd = NR + 4;                        // staged P row stride (floats)
   constexpr int kPsFloats = (kLdsBytes - kPst) / 4;
@@ -152,7 +170,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   float* blv = reinterpret_cast<float*>(smem + kBl);
   float* vl = reinterpret_cast<float*>(smem + kVl);
   float* wpl = reinterpret_cast<float*>(smem + kWp);
-  int32_t* plo = reinterpret_cast<int32_t*>(smem + kPlo);   // lo | hi | P base | E base
+  int32_t* plo = reinterpret_cast<int32_t*>(smem + kPlo);   // lo | hi | P | E | g base
   float* ylds = reinterpret_cast<float*>(smem + kYl);
   float* pst = reinterpret_cast<float*>(smem + kPst);
 
@@ -225,6 +243,9 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   // per case: a uniform branch per field between LDS and memory reads is
   // merged by the compiler into flat loads.
   const int ek = k / 2;   // bf16 table row in floats
+  // staged table rows 16 B apart in bank space (a row is 0 mod 64 banks), so
+  // the FM part's reads of different rows by one lane group do not conflict
+  const int ekp = ek + 4;
   bool allfit;
   {
     int used = 0;
@@ -233,8 +254,9 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       if (tid == 0) {
         plo[2 * kFusedMaxF + f] = used;
         plo[3 * kFusedMaxF + f] = used + span * kPsLd;
+        plo[4 * kFusedMaxF + f] = used + span * (kPsLd + ekp);
       }
-      used += span * (kPsLd + ek);
+      used += span * (kPsLd + ekp) + ((span + 3) & ~3);
     }
     allfit = used <= kPsFloats;
   }
@@ -251,8 +273,32 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       const float4* Ef = reinterpret_cast<const float4*>(
           reinterpret_cast<const float*>(a.E) + (int64_t)lo * ek);
       float4* dst = reinterpret_cast<float4*>(pst + used + span * kPsLd);
-      for (int x = tid; x < span * ek / 4; x += 256) dst[x] = Ef[x];
-      used += span * (kPsLd + ek);
+      // the copy also forms g[id] = Σ_k Wp_k·E[id][k]² of each staged row (the
+      // FM part's Σ_f e_f² term per table row): a row's 4·S0 chunks are
+      // consecutive lanes of one wave, summed by a butterfly
+      constexpr int CPR = 4 * S0;   // 16-B chunks per bf16 row (k = 32·S0)
+      static_assert((CPR & (CPR - 1)) == 0 && CPR <= kWave, "wide DeepFM kernel: k");
+      for (int x = tid; x < span * CPR; x += 256) {
+        const int row = x / CPR, c = x % CPR;
+        const float4 v = Ef[x];
+        dst[row * (ekp / 4) + c] = v;
+#if HHFM_WFM
+        const uint32_t u4[4] = {__float_as_uint(v.x), __float_as_uint(v.y),
+                                __float_as_uint(v.z), __float_as_uint(v.w)};
+        const float* wc = wpl + kFusedMaxF + 8 * c;
+        float g = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float e0 = __uint_as_float(u4[q] << 16), e1 = __uint_as_float(u4[q] & 0xffff0000u);
+          g += e0 * e0 * wc[2 * q];
+          g += e1 * e1 * wc[2 * q + 1];
+        }
+#pragma unroll
+        for (int o = CPR / 2; o >= 1; o >>= 1) g += __shfl_xor(g, o, kWave);
+        if (c == 0) pst[used + span * (kPsLd + ekp) + row] = g;
+#endif
+      }
+      used += span * (kPsLd + ekp) + ((span + 3) & ~3);
     }
   }
   dma_wait();
@@ -268,6 +314,23 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
       for (int f = 1; f < F; ++f) pid[rt][f] = ids[(row0 + 16 * rt) * F + f];
+    // staged blocks: LDS float offsets of the rows' P and table rows, and
+    // ½ Σ_f g[x_f] of the rows (lane group 0 adds it at the end)
+    int pb[3][F], eb[3][F];
+    float gh[3] = {0.f, 0.f, 0.f};
+    if constexpr (ST) {
+#pragma unroll
+      for (int f = 1; f < F; ++f) {
+        const int lo = plo[f], pofs = plo[2 * kFusedMaxF + f], eofs = plo[3 * kFusedMaxF + f];
+        const int gofs = plo[4 * kFusedMaxF + f];
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          pb[rt][f] = pofs + (pid[rt][f] - lo) * kPsLd;
+          eb[rt][f] = eofs + (pid[rt][f] - lo) * ekp;
+          if constexpr (HHFM_WFM) gh[rt] += pst[gofs + pid[rt][f] - lo];
+        }
+      }
+    }
 
     // FM second-order part (DFM.py:114-122) before layer 0: per k32 step,
     // the item's 8 columns 32s + 8kq .. +7 from its B operand, the other
@@ -292,8 +355,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
           uint4 u;
           if constexpr (ST)
             u = *reinterpret_cast<const uint4*>(
-                reinterpret_cast<const uint16_t*>(pst + plo[3 * kFusedMaxF + f2]) +
-                (pid[rt][f2] - plo[f2]) * k + 32 * s + 8 * kq);
+                reinterpret_cast<const uint16_t*>(pst + eb[rt][f2]) + 32 * s + 8 * kq);
           else
             u = *reinterpret_cast<const uint4*>(E + (int64_t)pid[rt][f2] * k + 32 * s + 8 * kq);
           const uint32_t u4[4] = {u.x, u.y, u.z, u.w};
@@ -301,9 +363,11 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
           for (int q = 0; q < 4; ++q) {
             const float u0 = __uint_as_float(u4[q] << 16), u1 = __uint_as_float(u4[q] & 0xffff0000u);
             fs[2 * q] += u0;
-            fq[2 * q] += u0 * u0;
             fs[2 * q + 1] += u1;
-            fq[2 * q + 1] += u1 * u1;
+            if constexpr (!(ST && HHFM_WFM)) {   // staged rows: Σ_k Wp_k·e_k² from g
+              fq[2 * q] += u0 * u0;
+              fq[2 * q + 1] += u1 * u1;
+            }
           }
         }
         const float4* wc = reinterpret_cast<const float4*>(wpl + kFusedMaxF + 32 * s + 8 * kq);
@@ -332,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         for (int rt = 0; rt < 3; ++rt) {
           const float* pp;
           if constexpr (ST)
-            pp = pst + plo[2 * kFusedMaxF + f] + (pid[rt][f] - plo[f]) * kPsLd + pos0;
+            pp = pst + pb[rt][f] + pos0;
           else
             pp = P + (f - 1) * a.proj_fstride + (int64_t)pid[rt][f] * a.proj_ld + pos0;
 #pragma unroll
@@ -347,6 +411,29 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       }
     };
 
+    // staged blocks: the P sums of layer-0 pass t+1 are formed during pass t's
+    // MFMA steps, unit (field f, row tile rt) in f-major order spread over the
+    // steps — per accumulator the same order of additions as psum
+    constexpr int kPU = NF * 3;
+    auto psum_part = [&](int t, int s, f32x4 (&acc)[3][2]) {
+      const int pos0 = 32 * t + 16 * (kq & 1) + 4 * (kq >> 1);
+#pragma unroll
+      for (int u = 0; u < kPU; ++u) {
+        if (u < s * kPU / S0 || u >= (s + 1) * kPU / S0) continue;
+        const int f = 1 + u / 3, rt = u % 3;
+        const float* pp = pst + pb[rt][f] + pos0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float4 x = *reinterpret_cast<const float4*>(pp + 8 * j);
+          acc[rt][j][0] += x.x;
+          acc[rt][j][1] += x.y;
+          acc[rt][j][2] += x.z;
+          acc[rt][j][3] += x.w;
+        }
+      }
+    };
+    f32x4 accN[3][2];
+
     static_for<0, NCH>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
       constexpr int layer = p / TM, t = p % TM;
@@ -357,12 +444,35 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       // this wave's DMAs of pass p+2: units wv, wv+4, ..., one per MFMA step
       const int Udma = p + 2 < NCH && !(HHFM_WKO & 8) ? cunits(p + 2) : 0;
       int dq = wv;
+      // the layer's bias (DFM.py:127) is the accumulators' initial value:
+      // units 32t + 16j + 4kq .. +3, the same for the three row tiles
+      const float* bl = blv + layer * NR + 32 * t + 4 * kq;
+      const f32x4 binit[2] = {*reinterpret_cast<const f32x4*>(bl),
+                              *reinterpret_cast<const f32x4*>(bl + 16)};
+      constexpr bool PI = ST && HHFM_WPI && !(HHFM_WKO & 2);   // interleaved P sums
       f32x4 acc[3][2];
+      if constexpr (layer == 0 && PI && t > 0) {
 #pragma unroll
-      for (int rt = 0; rt < 3; ++rt)
+        for (int rt = 0; rt < 3; ++rt)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (layer == 0 && !(HHFM_WKO & 2)) psum(t, acc);
+          for (int j = 0; j < 2; ++j) acc[rt][j] = accN[rt][j];
+      } else {
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[rt][j] = binit[j];
+        if constexpr (layer == 0 && !(HHFM_WKO & 2)) psum(t, acc);
+      }
+      constexpr bool PN = layer == 0 && PI && t + 1 < TM;   // this pass forms pass t+1's
+      if constexpr (PN) {
+        const float* bn = blv + 32 * (t + 1) + 4 * kq;
+        const f32x4 bnext[2] = {*reinterpret_cast<const f32x4*>(bn),
+                                *reinterpret_cast<const f32x4*>(bn + 16)};
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) accN[rt][j] = bnext[j];
+      }
       uint4 fa0 = wsl[0], fa1 = wsl[64];
 #pragma unroll
       for (int s = 0; s < S; ++s) {
@@ -389,6 +499,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
           acc[rt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b, acc[rt][1], 0, 0, 0);
 #endif
         }
+        if constexpr (PN) psum_part(t + 1, s, accN);
         if (dq < Udma) {
           dma_unit(p + 2, dq);
           dq += 4;
@@ -399,20 +510,19 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         dma_unit(p + 2, dq);
         dq += 4;
       }
-      const float* bl = blv + layer * NR + 32 * t + 4 * kq;
-      const float4 b0 = *reinterpret_cast<const float4*>(bl);
-      const float4 b1 = *reinterpret_cast<const float4*>(bl + 16);
       if constexpr (layer < 2) {
-        // bias + ReLU (DFM.py:127-128) + bf16: units 32t + 4kq .. +3 and
-        // 32t + 16 + 4kq .. +3 are lane group kq's k of step t next layer
+        // ReLU (DFM.py:128) + bf16: units 32t + 4kq .. +3 and 32t + 16 + 4kq
+        // .. +3 are lane group kq's k of step t next layer.  RNE first, then
+        // the ReLU on the packed pair as int16 max with 0 (a negative bf16 is
+        // a negative int16, and RNE keeps the sign): the same bits as
+        // rounding max(x, 0)
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt) {
           const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
-          const uint4 o = make_uint4(
-              pack_bf16x2(fmaxf(c0[0] + b0.x, 0.f), fmaxf(c0[1] + b0.y, 0.f)),
-              pack_bf16x2(fmaxf(c0[2] + b0.z, 0.f), fmaxf(c0[3] + b0.w, 0.f)),
-              pack_bf16x2(fmaxf(c1[0] + b1.x, 0.f), fmaxf(c1[1] + b1.y, 0.f)),
-              pack_bf16x2(fmaxf(c1[2] + b1.z, 0.f), fmaxf(c1[3] + b1.w, 0.f)));
+          const uint4 o = make_uint4(relu_bf16x2(pack_bf16x2(c0[0], c0[1])),
+                                     relu_bf16x2(pack_bf16x2(c0[2], c0[3])),
+                                     relu_bf16x2(pack_bf16x2(c1[0], c1[1])),
+                                     relu_bf16x2(pack_bf16x2(c1[2], c1[3])));
           if constexpr (layer == 0)
             X[rt][t] = o;
           else
@@ -426,14 +536,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt) {
           const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
-          part[rt] += fmaxf(c0[0] + b0.x, 0.f) * v0.x;
-          part[rt] += fmaxf(c0[1] + b0.y, 0.f) * v0.y;
-          part[rt] += fmaxf(c0[2] + b0.z, 0.f) * v0.z;
-          part[rt] += fmaxf(c0[3] + b0.w, 0.f) * v0.w;
-          part[rt] += fmaxf(c1[0] + b1.x, 0.f) * v1.x;
-          part[rt] += fmaxf(c1[1] + b1.y, 0.f) * v1.y;
-          part[rt] += fmaxf(c1[2] + b1.z, 0.f) * v1.z;
-          part[rt] += fmaxf(c1[3] + b1.w, 0.f) * v1.w;
+          part[rt] += fmaxf(c0[0], 0.f) * v0.x;
+          part[rt] += fmaxf(c0[1], 0.f) * v0.y;
+          part[rt] += fmaxf(c0[2], 0.f) * v0.z;
+          part[rt] += fmaxf(c0[3], 0.f) * v0.w;
+          part[rt] += fmaxf(c1[0], 0.f) * v1.x;
+          part[rt] += fmaxf(c1[1], 0.f) * v1.y;
+          part[rt] += fmaxf(c1[2], 0.f) * v1.z;
+          part[rt] += fmaxf(c1[3], 0.f) * v1.w;
           pin(part[rt]);
         }
       }
@@ -448,6 +558,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       yy += __shfl_xor(yy, 32, kWave);
       const int row = row0 + 16 * rt;
       const int64_t m = m0 + row;
+      if constexpr (ST && HHFM_WFM) yy -= 0.5f * gh[rt];   // − ½ Σ_f g[x_f], staged fields
       if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
     }
   };
