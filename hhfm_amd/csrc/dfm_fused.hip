@@ -1182,6 +1182,16 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + part;
 }
 
+// the FM part's per-element steps, spelled out (fused or not) so the two
+// kernels below round identically
+HHFM_DEV void fmb_acc(float& s, float& q, float v) {
+  s += v;
+  q = __fmaf_rn(v, v, q);
+}
+HHFM_DEV float fmb_term(float y, float s, float q, float wp) {
+  return __fmaf_rn(0.5f * __fmaf_rn(s, s, -q), wp, y);
+}
+
 // base[m] = ((Σ_f w[x_f]·Wp[f] + Σ_c ½((Σ_f e_fc)² − Σ_f e_fc²)·Wp[F+c]) + bp)
 // (DFM.py:109-122, 132-137 without the deep part): 16 lanes per row, 16-B
 // column chunks, at full occupancy — the FM part's table reads are latency-
@@ -1228,10 +1238,7 @@ __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ i
             }
           }
 #pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            s4[j][x] += v[x];
-            q4[j][x] += v[x] * v[x];
-          }
+          for (int x = 0; x < 4; ++x) fmb_acc(s4[j][x], q4[j][x], v[x]);
         }
       }
       if (live)
@@ -1239,15 +1246,121 @@ __global__ __launch_bounds__(256) void dfm_fm_base(const int32_t* __restrict__ i
         for (int j = 0; j < J; ++j)
 #pragma unroll
           for (int x = 0; x < 4; ++x)
-            y2 += 0.5f * (s4[j][x] * s4[j][x] - q4[j][x]) * Wp[F + c00 + 64 * j + 4 * sub + x];
+            y2 = fmb_term(y2, s4[j][x], q4[j][x], Wp[F + c00 + 64 * j + 4 * sub + x]);
     }
     y2 = group_sum<16>(y2);
     if (sub == 0) {
       float y1 = 0.f;
-      for (int f = 0; f < F; ++f) y1 += w[clamp_id(p[f], M)] * Wp[f];
+      for (int f = 0; f < F; ++f) y1 = __fmaf_rn(w[clamp_id(p[f], M)], Wp[f], y1);
       base[m] = (y1 + y2) + bp;
     }
   }
+}
+
+// dfm_fm_base over blocks of kFmbRows consecutive rows (rows grouped by user):
+// every field whose ids span few table rows in the block (the user and the
+// contexts) has those rows copied to LDS once, so only the item's row of each
+// row is read from the cache hierarchy (the grid-stride kernel above read all
+// F rows of every row through L1/L2: L1-bandwidth-bound).  Same arithmetic in
+// the same order per row — the same bits.
+constexpr int kFmbRows = 256;
+constexpr int kFmbStageB = 32 * 1024;
+template <bool TBF, int KJ>
+__global__ __launch_bounds__(256) void dfm_fm_base_st(const int32_t* __restrict__ idx, int64_t B,
+                                                      int F, const void* __restrict__ E,
+                                                      int64_t M, int k,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ Wp, float bp,
+                                                      float* __restrict__ base) {
+  static_assert(KJ > 0, "staged FM part: k % 64 == 0");
+  constexpr int ES = TBF ? 2 : 4;
+  __shared__ __attribute__((aligned(16))) char stage[kFmbStageB];
+  __shared__ int32_t sid[kFmbRows * kFusedMaxF];
+  __shared__ int32_t slo[kFusedMaxF], shi[kFusedMaxF], sbase[kFusedMaxF];
+  const int tid = threadIdx.x, sub = tid & 15;
+  const int64_t m0 = (int64_t)blockIdx.x * kFmbRows;
+  const int nr = (int)(B - m0 < kFmbRows ? B - m0 : kFmbRows);
+  if (tid < F) {
+    slo[tid] = 0x7fffffff;
+    shi[tid] = -1;
+  }
+  for (int x = tid; x < nr * F; x += 256) sid[x] = clamp_id(idx[m0 * F + x], M);
+  __syncthreads();
+  for (int x = tid; x < nr * F; x += 256) {
+    atomicMin(&slo[x % F], sid[x]);
+    atomicMax(&shi[x % F], sid[x]);
+  }
+  __syncthreads();
+  // staging plan (every thread computes the same): fields in order while
+  // their spans fit
+  const int rowb = k * ES, cap = kFmbStageB / rowb;
+  int used = 0;
+  for (int f = 0; f < F; ++f) {
+    const int span = shi[f] - slo[f] + 1;
+    const bool st = used + span <= cap;
+    if (tid == 0) sbase[f] = st ? used : -1;
+    used += st ? span : 0;
+  }
+  __syncthreads();
+  for (int f = 0; f < F; ++f) {
+    if (sbase[f] < 0) continue;
+    const int span = shi[f] - slo[f] + 1, c16 = rowb / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(E) +
+                                                      (int64_t)slo[f] * rowb);
+    uint4* dst = reinterpret_cast<uint4*>(stage + sbase[f] * rowb);
+    for (int x = tid; x < span * c16; x += 256) dst[x] = src[x];
+  }
+  __syncthreads();
+  for (int rr = tid / 16; rr < nr; rr += 16) {   // a row's 16 lanes stay together
+    const int32_t* p = sid + rr * F;
+    float y2 = 0.f;
+    float s4[KJ][4], q4[KJ][4];
+#pragma unroll
+    for (int j = 0; j < KJ; ++j)
+#pragma unroll
+      for (int x = 0; x < 4; ++x) { s4[j][x] = 0.f; q4[j][x] = 0.f; }
+#pragma unroll 4
+    for (int f = 0; f < F; ++f) {
+      const int id = p[f], sb = sbase[f];
+      const char* rowp = sb >= 0 ? stage + (sb + id - slo[f]) * rowb
+                                 : reinterpret_cast<const char*>(E) + (int64_t)id * rowb;
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) {
+        const int c0 = 64 * j + 4 * sub;
+        float v[4];
+        if constexpr (TBF) {
+          uint2 x;
+          if (sb >= 0) x = *reinterpret_cast<const uint2*>(stage + (sb + id - slo[f]) * rowb + c0 * 2);
+          else x = *reinterpret_cast<const uint2*>(rowp + c0 * 2);
+          v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+          v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+        } else {
+          float4 x;
+          if (sb >= 0) x = *reinterpret_cast<const float4*>(stage + (sb + id - slo[f]) * rowb + c0 * 4);
+          else x = *reinterpret_cast<const float4*>(rowp + c0 * 4);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) fmb_acc(s4[j][x], q4[j][x], v[x]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < KJ; ++j)
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        y2 = fmb_term(y2, s4[j][x], q4[j][x], Wp[F + 64 * j + 4 * sub + x]);
+    y2 = group_sum<16>(y2);
+    if (sub == 0) {
+      float y1 = 0.f;
+      for (int f = 0; f < F; ++f) y1 = __fmaf_rn(w[p[f]], Wp[f], y1);
+      base[m0 + rr] = (y1 + y2) + bp;
+    }
+  }
+}
+
+static bool dfm_fmb_staged() {   // HHFM_DFM_FMB_STAGE=0: the grid-stride kernel
+  const char* e = getenv("HHFM_DFM_FMB_STAGE");
+  return !(e && e[0] == '0');
 }
 
 static int fused_tm(int maxT) {
@@ -1437,7 +1550,24 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   else                                                                                     \
     hipLaunchKernelGGL((dfm_fm_base<false, KJ>), dim3((unsigned)fb), dim3(256), 0, st, idx,   \
                        B, F, E, M, k, w, Wp, bp, fm_base);
-        switch (k % 64 ? 0 : k / 64) {
+        const int kj = k % 64 ? 0 : k / 64;
+        const unsigned sblocks = (unsigned)((B + kFmbRows - 1) / kFmbRows);
+#define HHFM_FMBS(KJ)                                                                      \
+  if (tbf)                                                                                 \
+    hipLaunchKernelGGL((dfm_fm_base_st<true, KJ>), dim3(sblocks), dim3(256), 0, st, idx, B, \
+                       F, E, M, k, w, Wp, bp, fm_base);                                    \
+  else                                                                                     \
+    hipLaunchKernelGGL((dfm_fm_base_st<false, KJ>), dim3(sblocks), dim3(256), 0, st, idx,   \
+                       B, F, E, M, k, w, Wp, bp, fm_base);
+        if (dfm_fmb_staged() && kj > 0 && k * (tbf ? 2 : 4) <= kFmbStageB) {
+          switch (kj) {
+            case 1: HHFM_FMBS(1) break;
+            case 2: HHFM_FMBS(2) break;
+            case 4: HHFM_FMBS(4) break;
+            default: HHFM_FMBS(8) break;
+          }
+        } else
+        switch (kj) {
           case 1: HHFM_FMB(1) break;
           case 2: HHFM_FMB(2) break;
           case 4: HHFM_FMB(4) break;
@@ -1445,6 +1575,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
           default: HHFM_FMB(0) break;
         }
 #undef HHFM_FMB
+#undef HHFM_FMBS
       }
       a.fmbase = fm_base;
       {

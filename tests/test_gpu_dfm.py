@@ -365,6 +365,11 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
     unstaged = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                                proj=True).cpu().numpy()
     assert np.array_equal(unstaged, got)                 # same values, same order
+    monkeypatch.setenv("HHFM_DFM_FMB_STAGE", "0")        # FM part: grid-stride kernel
+    fmb = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                          proj=True).cpu().numpy()
+    assert np.array_equal(fmb, got)                      # staged rows: the same bits
+    monkeypatch.delenv("HHFM_DFM_FMB_STAGE")
     monkeypatch.setenv("HHFM_DFM_F32_WAVES", "4")        # 64-row workgroups
     w4 = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                          proj=True).cpu().numpy()
