@@ -1,13 +1,12 @@
 #!/bin/bash
-# C3 small-catalog path: kernel tests, then the bench C3 leg (3,000 queries and
-# the reference's 300-query call) with the query launch fused (default) and not.
+# catalog parity tests, then the C3 call timed with each library variant
+# (scripts/build_variants.sh into abw/<name>/), alternating twice
 cd "${GRAFT_REPO_ROOT:-.}"
-mkdir -p gpurun_out/c3
-timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/c3/pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/c3/pytest.log; exit 1; }
-tail -1 gpurun_out/c3/pytest.log
-for f in 1 0; do
-HHFM_CATALOG_FUSE_Q=$f timeout -k 10 300 python bench.py --legs c3 --cpu-seconds 0 --steps 2 --warmup 1 --rows 1048576 > gpurun_out/c3/b$f.json 2> gpurun_out/c3/b$f.err || exit 1
-python -c "
-import json; d=json.load(open('gpurun_out/c3/b$f.json'))['extra']['catalog_c3']
-print('fuse=$f', round(d['ms_per_query_batch']*1e3,1), 'us/3000q', round(d['reference_call_300_queries_us'],1), 'us/300q', d['parity']['parity'])"
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_models.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/c3ab_pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/c3ab_pytest.log; exit 1; }
+tail -1 gpurun_out/c3ab_pytest.log
+for rnd in 1 2; do
+for d in "$@"; do
+  cp $d/*.so hhfm_amd/lib/ && echo -n "$d " && timeout -k 10 120 python scripts/c3_trace.py 2>/dev/null || exit 1
+done
 done
