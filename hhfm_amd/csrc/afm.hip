@@ -424,6 +424,91 @@ __global__ __launch_bounds__(64) void afm_cat_prep(
   }
 }
 
+// The fused paths need only ufdot / suma: the same sums as afm_cat_prep, 4
+// waves per query, Wᵀ transposed into LDS once ([c][a]: lane a reads
+// consecutive words), the query pairs spread over the waves, each pair's
+// logits summed over c in afm_cat_prep's order; the per-wave Σ aij and
+// aij·pr terms are added in pair order by wave 0 (the same order as the
+// single-wave loop).
+constexpr int kAfmQsMaxPairs = 28;   // uF <= 8
+__global__ __launch_bounds__(256) void afm_cat_qside(
+    const int32_t* __restrict__ q, int64_t B, int F, const void* __restrict__ E, int t_bf16,
+    int64_t M, int k, const float* __restrict__ Wt, const float* __restrict__ ab,
+    const float* __restrict__ ap, int A, const float* __restrict__ P,
+    float* __restrict__ ufdot, float* __restrict__ suma) {
+  extern __shared__ __attribute__((aligned(16))) float qs[];   // afm_cat_qside_lds()
+  const int NA = (A + 63) / 64 * 64;
+  float* wt = qs;                        // [k][NA]
+  float* uf = wt + k * NA;               // [uF][k]
+  float* aij = uf + (F - 1) * k;         // [pairs]
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int uF = F - 1, np = uF * (uF - 1) / 2;
+  const int64_t b = blockIdx.x;
+  const int32_t* x = q + b * F;
+  for (int i = tid; i < uF * k; i += 256) {
+    const int f = i / k, c = i - f * k;
+    uf[i] = tab(E, t_bf16, clamp_id(x[f == 0 ? 0 : f + 1], M), k, c);
+  }
+  for (int i = tid; i < k * NA; i += 256) {
+    const int a = i / k, c = i - a * k;   // coalesced read of Wt[a][c]
+    wt[c * NA + a] = a < A ? Wt[(int64_t)a * k + c] : 0.f;
+  }
+  __syncthreads();
+  for (int pidx = wv; pidx < np; pidx += 4) {
+    int i = 0, rem = pidx;
+    while (rem >= uF - 1 - i) { rem -= uF - 1 - i; ++i; }
+    const int j = i + 1 + rem;
+    const float* ui = uf + i * k;
+    const float* uj = uf + j * k;
+    float lg = 0.f;
+    for (int a = l; a < A; a += 64) {
+      float acc = 0.f;
+      for (int c = 0; c < k; ++c) acc += (ui[c] * uj[c]) * wt[c * NA + a];
+      lg += ap[a] * fmaxf(acc + ab[a], 0.f);
+    }
+    lg = group_sum<kWave>(lg);
+    if (l == 0) aij[pidx] = expf(lg);     // raw exp, AFM.py:223
+  }
+  __syncthreads();
+  if (wv == 0) {
+    float uw[kAfmMaxK / 64];
+#pragma unroll
+    for (int r = 0; r < kAfmMaxK / 64; ++r) uw[r] = 0.f;
+    float sa = 0.f;
+    for (int pidx = 0, i = 0; i < uF; ++i)
+      for (int j = i + 1; j < uF; ++j, ++pidx) {
+        const float a = aij[pidx];
+        sa += a;
+#pragma unroll
+        for (int r = 0; r < kAfmMaxK / 64; ++r) {
+          const int c = l + 64 * r;
+          if (c < k) uw[r] += a * (uf[i * k + c] * uf[j * k + c]);   // UFwise, AFM.py:232
+        }
+      }
+    float ud = 0.f;
+#pragma unroll
+    for (int r = 0; r < kAfmMaxK / 64; ++r) {
+      const int c = l + 64 * r;
+      if (c < k) ud += P[c] * uw[r];
+    }
+    ud = group_sum<kWave>(ud);
+    if (l == 0) {
+      ufdot[b] = ud;
+      suma[b] = sa;
+    }
+  }
+}
+
+static size_t afm_cat_qside_lds(int F, int k, int A) {
+  const int NA = (A + 63) / 64 * 64;
+  return 4 * ((size_t)k * NA + (size_t)(F - 1) * k + kAfmQsMaxPairs);
+}
+
+static bool afm_cat_qside_on() {   // HHFM_AFM_QSIDE=0: afm_cat_prep
+  const char* e = getenv("HHFM_AFM_QSIDE");
+  return !(e && e[0] == '0');
+}
+
 // ---- A2 finish: wave per (query, 64-item block), lane = item -------------------
 __global__ __launch_bounds__(256) void afm_cat_finish(
     int64_t nq, int uF, int A, int G, const float* __restrict__ part, int64_t ldp,
@@ -663,6 +748,186 @@ __global__ __launch_bounds__(256) void afm_cat_fused(
   }
 }
 
+// ---- A2 per query: the query field folded into the attention weights -------
+// (uf_f ⊙ item)·W = item·(uf_f ⊙ W): a workgroup takes ONE query and a chunk of
+// item tiles, builds W''_f = uf_f ⊙ W (fp32, rounded once) for each of its
+// query fields and splits it into three bf16 LDS images once, so the item row
+// — the MFMA B operand — is split once per 16-k step for ALL fields (bf16
+// tables: it is its own single piece, 3 MFMAs per 16 k instead of 6), where
+// afm_cat_fused splits the pair product uf_f ⊙ item per field.  Likewise
+// P·(uf_f ⊙ item) = (P ⊙ uf_f)·item.  The products and the softmax / score
+// are AFM.py:227-243's; each term is rounded at a different place than
+// forming uf_f ⊙ item first (~1e-7 relative; tolerance 1e-5).
+template <int KS>
+static size_t afm_cat_w_lds(int F, int A) {
+  const int NA = (A + 31) / 32 * 32, uF = F - 1;
+  return (size_t)uF * 3 * NA * KS * 32 + (size_t)2 * uF * KS * 16 * 4 + 2 * NA * 4;
+}
+
+template <bool TBF, int NT, int KS>
+__global__ __launch_bounds__(512) void afm_cat_w(
+    const int32_t* __restrict__ q, int64_t nq, int F, const void* __restrict__ E, int64_t M,
+    const float* __restrict__ Wt, const float* __restrict__ att_b,
+    const float* __restrict__ att_p, int A, const float* __restrict__ P,
+    const float* __restrict__ ufdot, const float* __restrict__ suma, int64_t item_row_begin,
+    int32_t N, int tiles_per_block, int nchunk, const float* __restrict__ w,
+    float* __restrict__ scores) {
+  constexpr int NA = NT * 32, K = 16 * KS, U2 = K / 8;   // 16-B chunks per unit row
+  constexpr int SW2 = (U2 >= 16 ? 16 : U2 >= 8 ? 8 : U2 >= 4 ? 4 : U2 >= 2 ? 2 : 1) - 1;
+  constexpr int NP = TBF ? 1 : 3;                        // item pieces
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_cat_w_lds()
+  const int uF = F - 1;
+  uint4* imgb = reinterpret_cast<uint4*>(smem);          // [f][piece][unit][chunk]
+  float* Ql = smem + (size_t)uF * 3 * NA * U2 * 4;       // [f][K]: P ⊙ uf_f
+  float* ufs = Ql + uF * K;                              // [f][K]: uf_f
+  float* bl = ufs + uF * K;
+  float* apl = bl + NA;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int j = l & 31, h = l >> 5;
+  const int64_t b = blockIdx.x / nchunk;
+  const int chunk = (int)(blockIdx.x - b * nchunk);
+  // uf of the query: [E[q0], E[q2], ..., E[q_{F-1}]]  (AFM.py:210-212)
+  for (int x = tid; x < uF * K; x += 512) {
+    const int f = x / K, c = x - f * K;
+    const float v = tab(E, TBF, clamp_id(q[b * F + (f == 0 ? 0 : f + 1)], M), K, c);
+    ufs[x] = v;
+    Ql[x] = P[c] * v;
+  }
+  for (int x = tid; x < NA; x += 512) {
+    bl[x] = x < A ? att_b[x] : 0.f;
+    apl[x] = x < A ? att_p[x] : 0.f;
+  }
+  __syncthreads();
+  for (int x = tid; x < uF * NA * U2; x += 512) {
+    const int f = x / (NA * U2), r = x - f * NA * U2, u = r / U2, c = r - u * U2;
+    const int kb = 16 * (c >> 1) + 4 * (c & 1);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = u < A ? Wt[(int64_t)u * K + kb + e] * ufs[f * K + kb + e] : 0.f;
+      v[4 + e] = u < A ? Wt[(int64_t)u * K + kb + 8 + e] * ufs[f * K + kb + 8 + e] : 0.f;
+    }
+    bf16x8 p0, p1, p2;
+    split3x8(v, p0, p1, p2);
+    const int o = u * U2 + (c ^ (u & SW2));
+    imgb[(f * 3 + 0) * NA * U2 + o] = __builtin_bit_cast(uint4, p0);
+    imgb[(f * 3 + 1) * NA * U2 + o] = __builtin_bit_cast(uint4, p1);
+    imgb[(f * 3 + 2) * NA * U2 + o] = __builtin_bit_cast(uint4, p2);
+  }
+  __syncthreads();
+
+  const float ud = ufdot[b], sa = suma[b];
+  const int ntile = (N + 31) / 32;
+  const int t0 = chunk * tiles_per_block;
+  const int t1 = min(t0 + tiles_per_block, ntile);
+  // this lane's k of 16-k step t: {16t + 4h .. +3, 16t + 8 + 4h .. +3}
+  auto gather = [&](int tile, float (&x)[KS][8]) {
+    int32_t item = tile * 32 + j;
+    item = item < N ? item : 0;
+    const int64_t id = item_row_begin + item;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const int c0 = 16 * t + 4 * h;
+      if constexpr (TBF) {
+        const uint16_t* r = reinterpret_cast<const uint16_t*>(E) + id * K + c0;
+        const uint2 lo = *reinterpret_cast<const uint2*>(r), hi = *reinterpret_cast<const uint2*>(r + 8);
+        const uint32_t u4[4] = {lo.x, lo.y, hi.x, hi.y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[t][2 * e] = __uint_as_float(u4[e] << 16);
+          x[t][2 * e + 1] = __uint_as_float(u4[e] & 0xffff0000u);
+        }
+      } else {
+        const float* r = reinterpret_cast<const float*>(E) + id * K + c0;
+        const float4 lo = *reinterpret_cast<const float4*>(r), hi = *reinterpret_cast<const float4*>(r + 8);
+        x[t][0] = lo.x; x[t][1] = lo.y; x[t][2] = lo.z; x[t][3] = lo.w;
+        x[t][4] = hi.x; x[t][5] = hi.y; x[t][6] = hi.z; x[t][7] = hi.w;
+      }
+    }
+  };
+  // 8 waves, two per SIMD: a wave's gather and LDS waits overlap its
+  // partner's MFMAs (a register prefetch of the next row would cost the
+  // second wave)
+  for (int tile = t0 + wv; tile < t1; tile += 8) {
+    float xc[KS][8];
+    gather(tile, xc);
+    const int32_t item = tile * 32 + j;
+    // the item's pieces, once for every field
+    bf16x8 ip[NP][KS];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      if constexpr (TBF) {
+        u32x4_t u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = (__float_as_uint(xc[t][2 * e]) >> 16) | (__float_as_uint(xc[t][2 * e + 1]) & 0xffff0000u);
+        ip[0][t] = __builtin_bit_cast(bf16x8, u);
+      } else {
+        split3x8(xc[t], ip[0][t], ip[1][t], ip[2][t]);
+      }
+    }
+    float num = 0.f, den = 0.f;
+    for (int f = 0; f < uF; ++f) {
+      f32x16 acc[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int x = 0; x < 16; ++x) acc[n][x] = 0.f;
+      float sP = 0.f;
+      const uint4* fi = imgb + f * 3 * NA * U2;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        const int c0 = 16 * t + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sP = fmaf(xc[t][e], Ql[f * K + c0 + (e < 4 ? e : e + 4)], sP);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int u = 32 * n + j;
+          const int o = u * U2 + ((2 * t + h) ^ (u & SW2));
+          const bf16x8 a0 = __builtin_bit_cast(bf16x8, fi[o]);
+          const bf16x8 a1 = __builtin_bit_cast(bf16x8, fi[NA * U2 + o]);
+          const bf16x8 a2 = __builtin_bit_cast(bf16x8, fi[2 * NA * U2 + o]);
+          // smallest terms first (bf16 tables: the item is one piece)
+          if constexpr (!TBF) {
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, ip[2][t], acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, ip[1][t], acc[n], 0, 0, 0);
+          }
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, ip[0][t], acc[n], 0, 0, 0);
+          if constexpr (!TBF) acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, ip[1][t], acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, ip[0][t], acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, ip[0][t], acc[n], 0, 0, 0);
+        }
+      }
+      // field f: logit Σ_a p_a·relu(· + b_a), raw exp (AFM.py:227-230)
+      float lg = 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int u = 32 * n + 8 * g4 + 4 * h;
+          const float4 bq = *reinterpret_cast<const float4*>(bl + u);
+          const float4 pq = *reinterpret_cast<const float4*>(apl + u);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 0] + bq.x, 0.f), pq.x, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 1] + bq.y, 0.f), pq.y, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 2] + bq.z, 0.f), pq.z, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 3] + bq.w, 0.f), pq.w, lg);
+        }
+      lg += __shfl_xor(lg, 32, kWave);
+      sP += __shfl_xor(sP, 32, kWave);
+      const float a = expf(lg);
+      num = fmaf(a, sP, num);
+      den += a;
+    }
+    if (item < N && h == 0)
+      scores[b * N + item] = (ud + num) / (sa + den) + w[item_row_begin + item];
+  }
+}
+
+static bool afm_cat_w_on() {   // HHFM_AFM_CAT_W=0: afm_cat_fused
+  const char* e = getenv("HHFM_AFM_CAT_W");
+  return !(e && e[0] == '0');
+}
+
 static size_t afm_cat_fused_lds(int F, int k, int A, bool split) {
   const int NA = (A + 31) / 32 * 32;
   const size_t img = split ? (size_t)NA * k * 3 / 2 : (size_t)NA * k;
@@ -869,9 +1134,16 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   const int tb = dtype == HHFM_BF16;
   for (int64_t b0 = 0; b0 < B; b0 += p.qc) {
     const int64_t nq = (B - b0) < p.qc ? (B - b0) : p.qc;
-    hipLaunchKernelGGL(afm_cat_prep, dim3((unsigned)nq), dim3(64), 0, st, qidx + b0 * F, nq, F,
-                       E, tb, features_M, k, Wt, att_b, att_p, A, P, W2, D, ud, sa,
-                       (int)!p.fused);
+    const size_t qsl = afm_cat_qside_lds(F, k, A);
+    if (p.fused && afm_cat_qside_on() && uF * (uF - 1) / 2 <= kAfmQsMaxPairs &&
+        qsl <= 64 * 1024) {
+      hipLaunchKernelGGL(afm_cat_qside, dim3((unsigned)nq), dim3(256), qsl, st, qidx + b0 * F, nq,
+                         F, E, tb, features_M, k, Wt, att_b, att_p, A, P, ud, sa);
+    } else {
+      hipLaunchKernelGGL(afm_cat_prep, dim3((unsigned)nq), dim3(64), 0, st, qidx + b0 * F, nq, F,
+                         E, tb, features_M, k, Wt, att_b, att_p, A, P, W2, D, ud, sa,
+                         (int)!p.fused);
+    }
     if (p.fused) {
       const int64_t qgroups = (nq + 3) / 4;
       const int ntile = (item_count + 31) / 32;
@@ -882,6 +1154,53 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
       const dim3 grid((unsigned)(qgroups * nchunk));
       const int NT = (A + 31) / 32;
       const bool split = afm_split(F, k, A);
+      // per-query kernel: its W'' images fit (k <= 64), split arithmetic
+      const int KSw = k / 16;
+      bool wdone = false;
+      if (split && afm_cat_w_on() && k % 16 == 0 && KSw >= 1 && KSw <= 4) {
+        size_t wl = 0;
+        switch (KSw) {
+          case 1: wl = afm_cat_w_lds<1>(F, A); break;
+          case 2: wl = afm_cat_w_lds<2>(F, A); break;
+          case 3: wl = afm_cat_w_lds<3>(F, A); break;
+          default: wl = afm_cat_w_lds<4>(F, A); break;
+        }
+        if (wl <= 160 * 1024) {
+          int64_t nch = (1024 + nq - 1) / nq;
+          if (const char* e = getenv("HHFM_AFM_W_CH")) nch = atoi(e) > 0 ? atoi(e) : nch;   // A/B
+          const int64_t maxch = ntile / 32 > 1 ? ntile / 32 : 1;   // >= 4 tiles per wave
+          if (nch > maxch) nch = maxch;
+          const int tpw = (int)((ntile + nch - 1) / nch);
+          nch = (ntile + tpw - 1) / tpw;
+          const dim3 wgrid((unsigned)(nq * nch));
+#define HHFM_AFM_CAT_W_L(N, TB, KS)                                                              \
+  {                                                                                             \
+    allow_lds((const void*)afm_cat_w<TB, N, KS>, wl);                                            \
+    hipLaunchKernelGGL((afm_cat_w<TB, N, KS>), wgrid, dim3(512), wl, st, qidx + b0 * F, nq, F,   \
+                       E, features_M, Wt, att_b, att_p, A, P, ud, sa, (int64_t)item_row_begin,   \
+                       item_count, tpw, (int)nch, w, sc);                                        \
+    wdone = true;                                                                               \
+  }
+#define HHFM_AFM_CAT_W_K(N, TB)                                                                  \
+  switch (KSw) {                                                                                \
+    case 1: HHFM_AFM_CAT_W_L(N, TB, 1) break;                                                   \
+    case 2: HHFM_AFM_CAT_W_L(N, TB, 2) break;                                                   \
+    case 3: HHFM_AFM_CAT_W_L(N, TB, 3) break;                                                   \
+    default: HHFM_AFM_CAT_W_L(N, TB, 4) break;                                                  \
+  }
+#define HHFM_AFM_CAT_W(N)                                                                        \
+  if (NT == N) {                                                                                \
+    if (tb) { HHFM_AFM_CAT_W_K(N, true) } else { HHFM_AFM_CAT_W_K(N, false) }                   \
+  }
+          HHFM_AFM_CAT_W(1)
+          HHFM_AFM_CAT_W(2)
+          HHFM_AFM_CAT_W(3)
+          HHFM_AFM_CAT_W(4)
+#undef HHFM_AFM_CAT_W
+#undef HHFM_AFM_CAT_W_K
+#undef HHFM_AFM_CAT_W_L
+        }
+      }
       const size_t lds = afm_cat_fused_lds(F, k, A, split);
 #define HHFM_AFM_CAT_FUSED_L(N, TB, SP)                                                       \
   {                                                                                          \
@@ -891,7 +1210,7 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
                        (int64_t)item_row_begin, item_count, tpb, (int)nchunk, w, sc);          \
   }
 #define HHFM_AFM_CAT_FUSED(N)                                                                 \
-  if (NT == N) {                                                                             \
+  if (NT == N && !wdone) {                                                                   \
     if (tb) {                                                                                \
       if (split) HHFM_AFM_CAT_FUSED_L(N, true, true) else HHFM_AFM_CAT_FUSED_L(N, true, false) \
     } else {                                                                                 \
