@@ -54,7 +54,7 @@ def main():
     res = {
         "kernel": "fm_rows_fast<5,16,f32,w> (K1, hhfm_fm_score_rows)",
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) on "
-                  "scripts/pmc_fm_rows.py, gfx950, round 1; scripts/traffic_from_pmc.py",
+                  "scripts/pmc_fm_rows.py, gfx950; scripts/traffic_from_pmc.py",
         "pmc_rows": ROWS,
         "fetch_size_kb": fetch,
         "write_size_kb": write,
