@@ -1358,6 +1358,77 @@ __global__ __launch_bounds__(256) void dfm_fm_base_st(const int32_t* __restrict_
   }
 }
 
+// ---- the FM part from pair tables -------------------------------------------
+// Σ_k Wp_k·½((Σ_f e_fk)² − Σ_f e_fk²) = Σ_{f<g} Σ_k Wp_k·e_fk·e_gk
+// = Σ_{f<g} C[x_f][x_g] with C = (E ⊙ Wp)·Eᵀ over the table (DFM.py:114-122
+// re-associated): one exact-fp32 MFMA GEMM per call (2·M²·k flops) instead of
+// reading every row's F table rows.  Rows grouped by user: a block's user
+// rows of C are staged in LDS, the item's row of C is one line per row.
+constexpr int kFmpStageB = 48 * 1024;
+__global__ __launch_bounds__(256) void dfm_scale_rows(const void* __restrict__ E, int tbf,
+                                                      int64_t M, int k,
+                                                      const float* __restrict__ wk,
+                                                      float* __restrict__ out) {
+  const int64_t n = M * k;
+  for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+       x += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(x % k);
+    const float e = tbf ? __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(E)[x] << 16)
+                        : reinterpret_cast<const float*>(E)[x];
+    out[x] = e * wk[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restrict__ idx,
+                                                         int64_t B, int F, int64_t M,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ Wp, float bp,
+                                                         const float* __restrict__ C,
+                                                         float* __restrict__ base) {
+  __shared__ __attribute__((aligned(16))) float cst[kFmpStageB / 4];
+  __shared__ int32_t lohi[2];
+  const int tid = threadIdx.x;
+  const int64_t m = (int64_t)blockIdx.x * 256 + tid;
+  const bool live = m < B;
+  int32_t x[kFusedMaxF];
+  for (int f = 0; f < F; ++f) x[f] = live ? clamp_id(idx[m * F + f], M) : 0;
+  if (tid == 0) {
+    lohi[0] = 0x7fffffff;
+    lohi[1] = -1;
+  }
+  __syncthreads();
+  if (live) {
+    atomicMin(&lohi[0], x[0]);
+    atomicMax(&lohi[1], x[0]);
+  }
+  __syncthreads();
+  const int lo = lohi[0], span = lohi[1] - lo + 1;
+  const bool st = span > 0 && (int64_t)span * M * 4 <= kFmpStageB;
+  if (st) {   // field 0's rows of C (the block's user or two)
+    const float4* src = reinterpret_cast<const float4*>(C + (int64_t)lo * M);
+    const int64_t n = (int64_t)span * M;
+    if ((M & 3) == 0) {
+      for (int64_t i = tid; i < n / 4; i += 256) reinterpret_cast<float4*>(cst)[i] = src[i];
+    } else {
+      for (int64_t i = tid; i < n; i += 256) cst[i] = C[(int64_t)lo * M + i];
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  float y2 = 0.f;
+  for (int f = 0; f < F; ++f)
+    for (int g = f + 1; g < F; ++g)
+      y2 += (f == 0 && st) ? cst[(int64_t)(x[0] - lo) * M + x[g]] : C[(int64_t)x[f] * M + x[g]];
+  float y1 = 0.f;
+  for (int f = 0; f < F; ++f) y1 = __fmaf_rn(w[x[f]], Wp[f], y1);
+  base[m] = (y1 + y2) + bp;
+}
+
+static bool dfm_fm_pairs_on() {   // HHFM_DFM_FM_PAIRS=0: the row-reading pre-kernels
+  const char* e = getenv("HHFM_DFM_FM_PAIRS");
+  return !(e && e[0] == '0');
+}
+
 static bool dfm_fmb_staged() {   // HHFM_DFM_FMB_STAGE=0: the grid-stride kernel
   const char* e = getenv("HHFM_DFM_FMB_STAGE");
   return !(e && e[0] == '0');
@@ -1505,7 +1576,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      uint64_t perm, const int32_t* order, float* fm_base, hipStream_t st) {
+                      uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
+                      size_t scratch_bytes, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -1539,7 +1611,32 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
     if (split) {
       if (!fm_base) return false;
-      {
+      // FM part from the pair table C = (E ⊙ Wp)·Eᵀ when it and E ⊙ Wp fit the
+      // scratch, the table is small against the rows (the GEMM costs M² rows
+      // of k) and the ids fit int32 products
+      const size_t cbytes = (size_t)M * M * 4, sbytes = (size_t)M * k * 4;
+      if (dfm_fm_pairs_on() && scratch && M <= 32768 && (int64_t)M * 16 <= B &&
+          cbytes + sbytes + 512 <= scratch_bytes) {
+        float* Cp = reinterpret_cast<float*>(scratch);
+        float* Es = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) +
+                                             ((cbytes + 255) & ~size_t(255)));
+        hipLaunchKernelGGL(dfm_scale_rows, dim3(1024), dim3(256), 0, st, E, (int)tbf, M, k,
+                           Wp + F, Es);
+        GemmArgs g{};
+        g.M = M;
+        g.N = (int)M;
+        g.K = k;
+        g.A = Es;
+        g.lda = k;
+        g.Bt = E;
+        g.ldb = k;
+        g.b_src_bf16 = tbf;
+        g.C = Cp;
+        g.ldc = M;
+        launch_gemm(g, false, 0, st);
+        hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
+                           idx, B, F, M, w, Wp, bp, Cp, fm_base);
+      } else {
         const int64_t rows_per_block = 256 / 16;
         int64_t fb = (B + rows_per_block - 1) / rows_per_block;
         if (fb > 8192) fb = 8192;

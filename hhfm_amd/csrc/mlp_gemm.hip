@@ -30,7 +30,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
-                      uint64_t perm, const int32_t* order, float* fm_base, hipStream_t st);
+                      uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
+                      size_t scratch_bytes, hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
@@ -246,7 +247,8 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
   if ((proj || !layered) && p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
                        Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order,
-                       reinterpret_cast<float*>(ws + p.off_base), st))
+                       reinterpret_cast<float*>(ws + p.off_base), ws + p.off_h0,
+                       p.off_pack - p.off_h0, st))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);

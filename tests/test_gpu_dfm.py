@@ -365,11 +365,17 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
     unstaged = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                                proj=True).cpu().numpy()
     assert np.array_equal(unstaged, got)                 # same values, same order
-    monkeypatch.setenv("HHFM_DFM_FMB_STAGE", "0")        # FM part: grid-stride kernel
+    # FM part read from the rows (HHFM_DFM_FM_PAIRS=0) instead of the pair
+    # table C = (E ⊙ Wp)·Eᵀ: staged and grid-stride kernels give the same bits
+    monkeypatch.setenv("HHFM_DFM_FM_PAIRS", "0")
+    rows_fm = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                              proj=True).cpu().numpy()
+    monkeypatch.setenv("HHFM_DFM_FMB_STAGE", "0")
     fmb = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                           proj=True).cpu().numpy()
-    assert np.array_equal(fmb, got)                      # staged rows: the same bits
+    assert np.array_equal(fmb, rows_fm)
     monkeypatch.delenv("HHFM_DFM_FMB_STAGE")
+    monkeypatch.delenv("HHFM_DFM_FM_PAIRS")
     monkeypatch.setenv("HHFM_DFM_F32_WAVES", "4")        # 64-row workgroups
     w4 = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                          proj=True).cpu().numpy()
@@ -384,7 +390,8 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
                             proj=True).cpu().numpy()
     ref = orc.dfm_out(X, E, w, Ls, Bs, Wp, bp)[:, 0]
     mag = _magnitude(X, E, w, Ls, Bs, Wp, bp)
-    for name, v in (("grouped", got), ("ungrouped", flat), ("exact", exact)):
+    for name, v in (("grouped", got), ("ungrouped", flat), ("exact", exact),
+                    ("fm rows", rows_fm)):
         err = np.abs(v - ref) / mag
         assert np.all(err <= 2e-5), (name, float(err.max()))
     assert np.array_equal(again, got[perm])
