@@ -594,12 +594,15 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
     # the M table rows (exact-fp32 MFMA GEMM [M,256]x[256,5x400]) + the hidden
     # layers per row (split-bf16: each fp32 product = six bf16 MFMA products,
     # so their ceiling is the bf16 peak / 6) + the FM part and the last dot
-    ex = 2.0 * 5 * M * 256 * 400 + rows * (2.0 * 2 * 400 * 400 + 2.0 * (5 * 416 + 256 + 400))
+    # (+ the FM part's pair table C = (E ⊙ Wp)·Eᵀ, one [M, 256] x [256, M] GEMM)
+    ex = (2.0 * 5 * M * 256 * 400 + 2.0 * M * M * 256
+          + rows * (2.0 * 2 * 400 * 400 + 2.0 * (5 * 416 + 256 + 400)))
     split_peak = 2500.0 / 6
     return {"workload": "C5 (configs[4]) at the reference numerics: DeepFM F=5 k=256 + MLP "
                         "3x400, fp32-faithful: projected layer 0 (P by exact-fp32 MFMA inside "
                         "every step), hidden layers on split-bf16 MFMA (x = x0+x1+x2 exactly, "
-                        "the six piece products of order >= 2^-16, fp32 accumulation), rows "
+                        "the six piece products of order >= 2^-16, fp32 accumulation), FM part "
+                        "from the pair table (E*Wp)E^T (exact-fp32 MFMA inside every step), rows "
                         f"grouped by user, Frappe vocabulary, rows sharded {rows:,} per GPU",
             "ranks": world, "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms,
             "kernel_ms": kern,
