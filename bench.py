@@ -568,17 +568,20 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
         # executed (AUTO = ITEM): the projection of the M table rows for the 4
         # non-item fields, then the item field of layer 0 and the hidden
         # layers per row
-        ex = 2.0 * 4 * M * 256 * 400 + rows * (2.0 * (256 * 400 + 2 * 400 * 400)
-                                               + 2.0 * (5 + 256 + 400))
+        # (+ the FM part's pair table C = (E ⊙ Wp)·Eᵀ, one [M, 256] x [256, M] GEMM)
+        ex = (2.0 * 4 * M * 256 * 400 + 2.0 * M * M * 256
+              + rows * (2.0 * (256 * 400 + 2 * 400 * 400) + 2.0 * (5 + 256 + 400)))
         return {"workload": "C5 (configs[4]): DeepFM F=5 k=256 + MLP 3x400 (bf16 table as "
                             "SURVEY §8d prices it, bf16 MFMA, fp32 accumulation and FM part; "
-                            "layer 0 of every field but the item projected and the rows "
-                            "grouped by user inside every step), "
+                            "layer 0 of every field but the item projected, the FM part from "
+                            "the pair table (E*Wp)E^T and the rows grouped by user inside "
+                            "every step), "
                             f"Frappe vocabulary, rows sharded {rows:,} per GPU", "ranks": world,
                 "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
                 "executed_TFLOPs": ex / (kern * 1e-3) / 1e12,
-                "kernel": "dfm_fused_w<13,8,4> (dfm_wide.hip: 192 rows per workgroup, 48 per "
-                          "wave) after the user grouping, the projection and the weight packing",
+                "kernel": "dfm_fused_w<13,8,4,true> (dfm_wide.hip: 192 rows per workgroup, 48 "
+                          "per wave) after the user grouping, the projection, the FM pair table "
+                          "and the weight packing",
                 "roofline": {"bound": "mfma", "executed_flops_per_pass": ex,
                              "achieved_TFLOPs": ex / (kern * 1e-3) / 1e12,
                              "peak_TFLOPs": 2500.0,

@@ -51,6 +51,10 @@ struct FusedDfmArgs {
   // stage: P rows of narrow-span fields staged in LDS (HHFM_DFM_F32_STAGE=0: off)
   const float* fmbase;
   int stage;
+  // scratch for the FM part's pair table (dfm_fm_pairs); fm_out: its output
+  void* scratch;
+  size_t scratch_bytes;
+  float* fm_out;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -91,5 +95,9 @@ struct BoolC {
 // the 256-row kernel (dfm_wide.hip) at an instantiated shape; false: not
 // instantiated (the caller runs dfm_fused)
 bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st);
+// base[m] = (Σ_f w·Wp + FM part) + bp into a.fm_out from the pair table
+// C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip); false (nothing launched) when it does not
+// fit a.scratch or the rows are too few to pay for it
+bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st);
 
 }  // namespace hhfm

@@ -1429,6 +1429,35 @@ static bool dfm_fm_pairs_on() {   // HHFM_DFM_FM_PAIRS=0: the row-reading pre-ke
   return !(e && e[0] == '0');
 }
 
+bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
+  const int64_t M = a.M, B = a.B;
+  const int k = a.k;
+  const size_t cbytes = (size_t)M * M * 4, sbytes = (size_t)M * k * 4;
+  if (!dfm_fm_pairs_on() || !a.scratch || !a.fm_out || M > 32768 || M * 16 > B ||
+      k % 4 || cbytes + sbytes + 512 > a.scratch_bytes)
+    return false;
+  float* Cp = reinterpret_cast<float*>(a.scratch);
+  float* Es = reinterpret_cast<float*>(reinterpret_cast<char*>(a.scratch) +
+                                       ((cbytes + 255) & ~size_t(255)));
+  hipLaunchKernelGGL(dfm_scale_rows, dim3(1024), dim3(256), 0, st, a.E, (int)tbf, M, k,
+                     a.Wp + a.F, Es);
+  GemmArgs g{};
+  g.M = M;
+  g.N = (int)M;
+  g.K = k;
+  g.A = Es;
+  g.lda = k;
+  g.Bt = a.E;
+  g.ldb = k;
+  g.b_src_bf16 = tbf;
+  g.C = Cp;
+  g.ldc = M;
+  launch_gemm(g, false, 0, st);
+  hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
+                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out);
+  return true;
+}
+
 static bool dfm_fmb_staged() {   // HHFM_DFM_FMB_STAGE=0: the grid-stride kernel
   const char* e = getenv("HHFM_DFM_FMB_STAGE");
   return !(e && e[0] == '0');
@@ -1602,6 +1631,9 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.Fd = pj ? proj_from : F;
   a.perm = perm;
   a.order = order;
+  a.scratch = scratch;
+  a.scratch_bytes = scratch_bytes;
+  a.fm_out = fm_base;
   if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
     // the fp32 kernel projects all fields, in the caller's order
@@ -1611,31 +1643,9 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
     if (split) {
       if (!fm_base) return false;
-      // FM part from the pair table C = (E ⊙ Wp)·Eᵀ when it and E ⊙ Wp fit the
-      // scratch, the table is small against the rows (the GEMM costs M² rows
-      // of k) and the ids fit int32 products
-      const size_t cbytes = (size_t)M * M * 4, sbytes = (size_t)M * k * 4;
-      if (dfm_fm_pairs_on() && scratch && M <= 32768 && (int64_t)M * 16 <= B &&
-          cbytes + sbytes + 512 <= scratch_bytes) {
-        float* Cp = reinterpret_cast<float*>(scratch);
-        float* Es = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) +
-                                             ((cbytes + 255) & ~size_t(255)));
-        hipLaunchKernelGGL(dfm_scale_rows, dim3(1024), dim3(256), 0, st, E, (int)tbf, M, k,
-                           Wp + F, Es);
-        GemmArgs g{};
-        g.M = M;
-        g.N = (int)M;
-        g.K = k;
-        g.A = Es;
-        g.lda = k;
-        g.Bt = E;
-        g.ldb = k;
-        g.b_src_bf16 = tbf;
-        g.C = Cp;
-        g.ldc = M;
-        launch_gemm(g, false, 0, st);
-        hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
-                           idx, B, F, M, w, Wp, bp, Cp, fm_base);
+      // FM part from the pair table C = (E ⊙ Wp)·Eᵀ (dfm_fm_pairs) when it fits
+      // and pays; otherwise from the rows
+      if (dfm_fm_pairs(a, tbf, st)) {
       } else {
         const int64_t rows_per_block = 256 / 16;
         int64_t fb = (B + rows_per_block - 1) / rows_per_block;

@@ -147,8 +147,10 @@ __global__ __launch_bounds__(256) void dfm_pack_weights_w(FusedDfmArgs a, int TM
   }
 }
 
-template <int TM, int S0, int NF>
+template <int TM, int S0, int NF, bool PAIRS>
 __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
+  // PAIRS: a.fmbase[m] = (Σ_f w·Wp + FM part) + bp from the pair table
+  // (dfm_fm_pairs), so no table rows are staged and no FM part runs here
   static_assert(NF >= 1 && NF < kFusedMaxF, "wide DeepFM kernel: fields");
   constexpr int F = NF + 1;
   constexpr int NR = TM * 32;
@@ -221,7 +223,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     for (int s = 0; s < S0; ++s)
       E0[rt][s] = *reinterpret_cast<const uint4*>(E + id * k + 32 * s + 8 * kq);
   }
-  if (tid < kWideRows) {   // Σ_f w[x_f]·Wp[f], one row per thread (dfm_fused's order)
+  if (!PAIRS && tid < kWideRows) {   // Σ_f w[x_f]·Wp[f], one row per thread (dfm_fused's order)
     float wv8[kFusedMaxF];
 #pragma unroll
     for (int f = 0; f < kFusedMaxF; ++f) wv8[f] = f < F ? a.w[ids[tid * F + f]] : 0.f;
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   const int ek = k / 2;   // bf16 table row in floats
   // staged table rows 16 B apart in bank space (a row is 0 mod 64 banks), so
   // the FM part's reads of different rows by one lane group do not conflict
-  const int ekp = ek + 4;
+  const int ekp = PAIRS ? 0 : ek + 4;
   bool allfit;
   {
     int used = 0;
@@ -256,7 +258,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         plo[3 * kFusedMaxF + f] = used + span * kPsLd;
         plo[4 * kFusedMaxF + f] = used + span * (kPsLd + ekp);
       }
-      used += span * (kPsLd + ekp) + ((span + 3) & ~3);
+      used += span * (kPsLd + ekp) + (PAIRS ? 0 : ((span + 3) & ~3));
     }
     allfit = used <= kPsFloats;
   }
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       // consecutive lanes of one wave, summed by a butterfly
       constexpr int CPR = 4 * S0;   // 16-B chunks per bf16 row (k = 32·S0)
       static_assert((CPR & (CPR - 1)) == 0 && CPR <= kWave, "wide DeepFM kernel: k");
-      for (int x = tid; x < span * CPR; x += 256) {
+      for (int x = tid; x < (PAIRS ? 0 : span * CPR); x += 256) {
         const int row = x / CPR, c = x % CPR;
         const float4 v = Ef[x];
         dst[row * (ekp / 4) + c] = v;
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         if (c == 0) pst[used + span * (kPsLd + ekp) + row] = g;
 #endif
       }
-      used += span * (kPsLd + ekp) + ((span + 3) & ~3);
+      used += span * (kPsLd + ekp) + (PAIRS ? 0 : ((span + 3) & ~3));
     }
   }
   dma_wait();
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         for (int rt = 0; rt < 3; ++rt) {
           pb[rt][f] = pofs + (pid[rt][f] - lo) * kPsLd;
           eb[rt][f] = eofs + (pid[rt][f] - lo) * ekp;
-          if constexpr (HHFM_WFM) gh[rt] += pst[gofs + pid[rt][f] - lo];
+          if constexpr (HHFM_WFM && !PAIRS) gh[rt] += pst[gofs + pid[rt][f] - lo];
         }
       }
     }
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     // the item's 8 columns 32s + 8kq .. +7 from its B operand, the other
     // fields' from their rows; lane groups summed at the end
 #pragma unroll
-    for (int s = 0; s < ((HHFM_WKO & 1) ? 0 : S0); ++s) {
+    for (int s = 0; s < ((HHFM_WKO & 1) || PAIRS ? 0 : S0); ++s) {
 #pragma unroll
       for (int rt = 0; rt < 3; ++rt) {
         const uint4 ex = E0[rt][s];
@@ -558,8 +560,11 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       yy += __shfl_xor(yy, 32, kWave);
       const int row = row0 + 16 * rt;
       const int64_t m = m0 + row;
-      if constexpr (ST && HHFM_WFM) yy -= 0.5f * gh[rt];   // − ½ Σ_f g[x_f], staged fields
-      if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
+      if constexpr (ST && HHFM_WFM && !PAIRS) yy -= 0.5f * gh[rt];   // − ½ Σ_f g[x_f], staged fields
+      if (kq == 0 && m < a.B) {
+        if constexpr (PAIRS) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + pt;
+        else a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
+      }
     }
   };
   if (allfit) body(BoolC<true>{});
@@ -578,7 +583,13 @@ bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st) {
 #define HHFM_WIDE(T, A, N)                                                                 \
   if (TM == T && S0 == A && a.F == N + 1) {                                                \
     hipLaunchKernelGGL(dfm_pack_weights_w, dim3(pblocks), dim3(256), 0, st, a, T, A, packed); \
-    hipLaunchKernelGGL((dfm_fused_w<T, A, N>), grid, dim3(256), 0, st, a);                 \
+    if (dfm_fm_pairs(a, true, st)) {                                                       \
+      FusedDfmArgs b = a;                                                                  \
+      b.fmbase = a.fm_out;                                                                 \
+      hipLaunchKernelGGL((dfm_fused_w<T, A, N, true>), grid, dim3(256), 0, st, b);         \
+    } else {                                                                               \
+      hipLaunchKernelGGL((dfm_fused_w<T, A, N, false>), grid, dim3(256), 0, st, a);        \
+    }                                                                                      \
     return true;                                                                           \
   }
   HHFM_WIDE(13, 8, 4)   // C5: F = 5, k = 256, 3 x 400
