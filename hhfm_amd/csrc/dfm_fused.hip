@@ -1384,7 +1384,7 @@ __global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restri
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ Wp, float bp,
                                                          const float* __restrict__ C,
-                                                         float* __restrict__ base) {
+                                                         float* __restrict__ base, int stage) {
   __shared__ __attribute__((aligned(16))) float cst[kFmpStageB / 4];
   __shared__ int32_t lohi[2];
   const int tid = threadIdx.x;
@@ -1403,7 +1403,7 @@ __global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restri
   }
   __syncthreads();
   const int lo = lohi[0], span = lohi[1] - lo + 1;
-  const bool st = span > 0 && (int64_t)span * M * 4 <= kFmpStageB;
+  const bool st = stage && span > 0 && (int64_t)span * M * 4 <= kFmpStageB;
   if (st) {   // field 0's rows of C (the block's user or two)
     const float4* src = reinterpret_cast<const float4*>(C + (int64_t)lo * M);
     const int64_t n = (int64_t)span * M;
@@ -1453,8 +1453,12 @@ bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
   g.C = Cp;
   g.ldc = M;
   launch_gemm(g, false, 0, st);
+  static const int stage = [] {   // HHFM_DFM_PAIRS_STAGE=0: user rows of C from the caches
+    const char* e = getenv("HHFM_DFM_PAIRS_STAGE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
   hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
-                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out);
+                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out, stage);
   return true;
 }
 
