@@ -1362,8 +1362,8 @@ __global__ __launch_bounds__(256) void dfm_fm_base_st(const int32_t* __restrict_
 // Σ_k Wp_k·½((Σ_f e_fk)² − Σ_f e_fk²) = Σ_{f<g} Σ_k Wp_k·e_fk·e_gk
 // = Σ_{f<g} C[x_f][x_g] with C = (E ⊙ Wp)·Eᵀ over the table (DFM.py:114-122
 // re-associated): one exact-fp32 MFMA GEMM per call (2·M²·k flops) instead of
-// reading every row's F table rows.  Rows grouped by user: a block's user
-// rows of C are staged in LDS, the item's row of C is one line per row.
+// reading every row's F table rows.  Rows grouped by user: a block's entries
+// of its user's row of C stay in L1/L2; the item's are one line per row.
 constexpr int kFmpStageB = 48 * 1024;
 __global__ __launch_bounds__(256) void dfm_scale_rows(const void* __restrict__ E, int tbf,
                                                       int64_t M, int k,
@@ -1453,9 +1453,12 @@ bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
   g.C = Cp;
   g.ldc = M;
   launch_gemm(g, false, 0, st);
-  static const int stage = [] {   // HHFM_DFM_PAIRS_STAGE=0: user rows of C from the caches
+  // HHFM_DFM_PAIRS_STAGE=1: a block's user rows of C staged in LDS first (the
+  // same values; copying whole rows of C per block measured slower than
+  // gathering the few entries a block reads through L1/L2)
+  static const int stage = [] {
     const char* e = getenv("HHFM_DFM_PAIRS_STAGE");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
   }();
   hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
                      a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out, stage);

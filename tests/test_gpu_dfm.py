@@ -376,6 +376,11 @@ def test_dfm_f32_split_grouped(tdt, monkeypatch):
     assert np.array_equal(fmb, rows_fm)
     monkeypatch.delenv("HHFM_DFM_FMB_STAGE")
     monkeypatch.delenv("HHFM_DFM_FM_PAIRS")
+    monkeypatch.setenv("HHFM_DFM_PAIRS_STAGE", "1")     # user rows of C staged in LDS
+    pst = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
+                          proj=True).cpu().numpy()
+    assert np.array_equal(pst, got)
+    monkeypatch.delenv("HHFM_DFM_PAIRS_STAGE")
     monkeypatch.setenv("HHFM_DFM_F32_WAVES", "4")        # 64-row workgroups
     w4 = ops.dfm_forward(xd, m.table, wb, Wt, bs, dims, torch.float32, Wpd, bpd,
                          proj=True).cpu().numpy()
