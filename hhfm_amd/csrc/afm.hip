@@ -504,11 +504,6 @@ static size_t afm_cat_qside_lds(int F, int k, int A) {
   return 4 * ((size_t)k * NA + (size_t)(F - 1) * k + kAfmQsMaxPairs);
 }
 
-static bool afm_cat_qside_on() {   // HHFM_AFM_QSIDE=0: afm_cat_prep
-  const char* e = getenv("HHFM_AFM_QSIDE");
-  return !(e && e[0] == '0');
-}
-
 // ---- A2 finish: wave per (query, 64-item block), lane = item -------------------
 __global__ __launch_bounds__(256) void afm_cat_finish(
     int64_t nq, int uF, int A, int G, const float* __restrict__ part, int64_t ldp,
@@ -773,7 +768,9 @@ __global__ __launch_bounds__(512) void afm_cat_w(
     int32_t N, int tiles_per_block, int nchunk, const float* __restrict__ w,
     float* __restrict__ scores) {
   constexpr int NA = NT * 32, K = 16 * KS, U2 = K / 8;   // 16-B chunks per unit row
-  constexpr int SW2 = (U2 >= 16 ? 16 : U2 >= 8 ? 8 : U2 >= 4 ? 4 : U2 >= 2 ? 2 : 1) - 1;
+  // swizzle mask: the largest power of two (<= 16) that DIVIDES U2, so the
+  // XOR stays inside the unit's row (U2 = 6 at k = 48: mask 1, not 3)
+  constexpr int SW2 = ((U2 & -U2) < 16 ? (U2 & -U2) : 16) - 1;
   constexpr int NP = TBF ? 1 : 3;                        // item pieces
   extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_cat_w_lds()
   const int uF = F - 1;
@@ -923,11 +920,6 @@ __global__ __launch_bounds__(512) void afm_cat_w(
   }
 }
 
-static bool afm_cat_w_on() {   // HHFM_AFM_CAT_W=0: afm_cat_fused
-  const char* e = getenv("HHFM_AFM_CAT_W");
-  return !(e && e[0] == '0');
-}
-
 static size_t afm_cat_fused_lds(int F, int k, int A, bool split) {
   const int NA = (A + 31) / 32 * 32;
   const size_t img = split ? (size_t)NA * k * 3 / 2 : (size_t)NA * k;
@@ -935,22 +927,18 @@ static size_t afm_cat_fused_lds(int F, int k, int A, bool split) {
 }
 
 // fused A2 envelope: Wᵀ padded to NT*32 <= 128 rows, <= 7 query fields, the
-// Wᵀ image and the 4 queries' fields in LDS; HHFM_AFM_CATALOG_GEMM=1 forces the GEMM path.
-static bool afm_cat_fused_ok(int F, int k, int A) {
-  static const bool gemm = [] {
-    const char* e = getenv("HHFM_AFM_CATALOG_GEMM");
-    return e && e[0] == '1';
-  }();
+// Wᵀ image and the 4 queries' fields in LDS; HHFM_PLAN_GEMM forces the GEMM path.
+static bool afm_cat_fused_ok(int F, int k, int A, int32_t plan) {
   const int NT = (A + 31) / 32;
-  return !gemm && F - 1 <= kAfmCatFusedMaxUF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 &&
+  return !(plan & HHFM_PLAN_GEMM) && F - 1 <= kAfmCatFusedMaxUF && k % 8 == 0 && k <= kAfmMaxK && NT <= 4 &&
          afm_cat_fused_lds(F, k, A, false) <= 160 * 1024;
 }
 
 // split-bf16 variant of the fused kernels: k % 16 == 0, its LDS images fit,
-// and HHFM_AFM_EXACT != 1
-static bool afm_split(int F, int k, int A) {
-  const char* e = getenv("HHFM_AFM_EXACT");
-  return k % 16 == 0 && !(e && e[0] == '1') && afm_cat_fused_lds(F, k, A, true) <= 160 * 1024;
+// and no HHFM_PLAN_EXACT_FP32
+static bool afm_split(int F, int k, int A, int32_t plan) {
+  return k % 16 == 0 && !(plan & HHFM_PLAN_EXACT_FP32) &&
+         afm_cat_fused_lds(F, k, A, true) <= 160 * 1024;
 }
 
 struct AfmCatPlan {
@@ -960,10 +948,11 @@ struct AfmCatPlan {
   size_t off_W2, off_D, off_ud, off_sa, off_part, off_sc, total;
 };
 
-static AfmCatPlan afm_cat_plan(int64_t B, int F, int k, int A, int N, int64_t max_cols) {
+static AfmCatPlan afm_cat_plan(int64_t B, int F, int k, int A, int N, int64_t max_cols,
+                               int32_t plan) {
   AfmCatPlan p{};
   const int uF = F - 1;
-  p.fused = afm_cat_fused_ok(F, k, A);
+  p.fused = afm_cat_fused_ok(F, k, A, plan);
   if (p.fused) {   // only Σa_uf, P·ufw and the [qc, N] score block
     int64_t qc = max_cols / ((int64_t)uF * A);
     if (qc < 1) qc = 1;
@@ -1011,6 +1000,17 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
                                 float w0, const float* Wt, const float* att_b,
                                 const float* att_p, int32_t A, const float* P, float* out,
                                 void* workspace, size_t ws_bytes, void* stream) {
+  return hhfm_afm_forward_ex(idx, B, F, E, features_M, k, dtype, w, w0, Wt, att_b, att_p, A, P,
+                             out, HHFM_PLAN_DEFAULT, workspace, ws_bytes, stream);
+}
+
+extern "C" int hhfm_afm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                                   int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                                   float w0, const float* Wt, const float* att_b,
+                                   const float* att_p, int32_t A, const float* P, float* out,
+                                   int32_t plan, void* workspace, size_t ws_bytes,
+                                   void* stream) {
+  if (plan & ~HHFM_PLAN_ALL) return HHFM_EINVAL;
   if (B < 0 || F < 2 || F > 16 || k < 1 || A < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (k % 4) return HHFM_EUNSUPPORTED;
@@ -1029,8 +1029,7 @@ extern "C" int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const 
       int64_t blocks = (nblk + 3) / 4;
       if (blocks > 2048) blocks = 2048;
       const bool tb = dtype == HHFM_BF16;
-      const char* ex = getenv("HHFM_AFM_EXACT");   // "1": the fp32-MFMA kernel (A/B)
-      const bool split = k % 16 == 0 && !(ex && ex[0] == '1') &&
+      const bool split = k % 16 == 0 && !(plan & HHFM_PLAN_EXACT_FP32) &&
                          afm_rows_fused_lds(k, A, true) <= 160 * 1024;
       const size_t lds = afm_rows_fused_lds(k, A, split);
 #define HHFM_AFM_FUSED_K(N, TB, SP, KS)                                                      \
@@ -1095,7 +1094,17 @@ extern "C" int hhfm_afm_catalog_topk_workspace(int64_t B, int32_t F, int32_t k, 
                                                size_t* ws_bytes) {
   if (!ws_bytes || B < 0 || F < 3 || k < 1 || A < 1 || item_count < 1 || max_cols < 1)
     return HHFM_EINVAL;
-  *ws_bytes = afm_cat_plan(B, F, k, A, item_count, max_cols).total;
+  *ws_bytes = afm_cat_plan(B, F, k, A, item_count, max_cols, HHFM_PLAN_DEFAULT).total;
+  return HHFM_OK;
+}
+
+extern "C" int hhfm_afm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t k, int32_t A,
+                                                  int32_t item_count, int64_t max_cols,
+                                                  int32_t plan, size_t* ws_bytes) {
+  if (!ws_bytes || B < 0 || F < 3 || k < 1 || A < 1 || item_count < 1 || max_cols < 1 ||
+      (plan & ~HHFM_PLAN_ALL))
+    return HHFM_EINVAL;
+  *ws_bytes = afm_cat_plan(B, F, k, A, item_count, max_cols, plan).total;
   return HHFM_OK;
 }
 
@@ -1107,6 +1116,22 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
                                      int32_t global_item_base, int32_t K, int64_t max_cols,
                                      float* top_score, int32_t* top_idx, void* workspace,
                                      size_t ws_bytes, void* stream) {
+  return hhfm_afm_catalog_topk_ex(qidx, B, F, E, features_M, k, dtype, w, Wt, att_b, att_p, A,
+                                  P, item_row_begin, item_count, global_item_base, K, max_cols,
+                                  top_score, top_idx, HHFM_PLAN_DEFAULT, workspace, ws_bytes,
+                                  stream);
+}
+
+extern "C" int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F,
+                                        const void* E, int64_t features_M, int32_t k,
+                                        int32_t dtype, const float* w, const float* Wt,
+                                        const float* att_b, const float* att_p, int32_t A,
+                                        const float* P, int32_t item_row_begin,
+                                        int32_t item_count, int32_t global_item_base, int32_t K,
+                                        int64_t max_cols, float* top_score, int32_t* top_idx,
+                                        int32_t plan, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  if (plan & ~HHFM_PLAN_ALL) return HHFM_EINVAL;
   if (B < 0 || F < 3 || F - 1 > kAfmMaxUF || k < 1 || k > kAfmMaxK || A < 1 ||
       features_M < 1 || max_cols < 1)
     return HHFM_EINVAL;
@@ -1115,12 +1140,12 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
     return HHFM_EINVAL;
   if (K < 1 || K > item_count) return HHFM_EINVAL;
   if (K > 64) return HHFM_EUNSUPPORTED;
-  if (!afm_cat_fused_ok(F, k, A) && (k % 4 || A % 16 || (A > 64 && A % 64)))
+  if (!afm_cat_fused_ok(F, k, A, plan) && (k % 4 || A % 16 || (A > 64 && A % 64)))
     return HHFM_EUNSUPPORTED;
   if (B == 0) return HHFM_OK;
   if (!qidx || !E || !w || !Wt || !att_b || !att_p || !P || !top_score || !top_idx)
     return HHFM_EINVAL;
-  const AfmCatPlan p = afm_cat_plan(B, F, k, A, item_count, max_cols);
+  const AfmCatPlan p = afm_cat_plan(B, F, k, A, item_count, max_cols, plan);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   float* W2 = reinterpret_cast<float*>(ws + p.off_W2);
@@ -1135,7 +1160,7 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   for (int64_t b0 = 0; b0 < B; b0 += p.qc) {
     const int64_t nq = (B - b0) < p.qc ? (B - b0) : p.qc;
     const size_t qsl = afm_cat_qside_lds(F, k, A);
-    if (p.fused && afm_cat_qside_on() && uF * (uF - 1) / 2 <= kAfmQsMaxPairs &&
+    if (p.fused && uF * (uF - 1) / 2 <= kAfmQsMaxPairs &&
         qsl <= 64 * 1024) {
       hipLaunchKernelGGL(afm_cat_qside, dim3((unsigned)nq), dim3(256), qsl, st, qidx + b0 * F, nq,
                          F, E, tb, features_M, k, Wt, att_b, att_p, A, P, ud, sa);
@@ -1153,11 +1178,11 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
       nchunk = (ntile + tpb - 1) / tpb;
       const dim3 grid((unsigned)(qgroups * nchunk));
       const int NT = (A + 31) / 32;
-      const bool split = afm_split(F, k, A);
+      const bool split = afm_split(F, k, A, plan);
       // per-query kernel: its W'' images fit (k <= 64), split arithmetic
       const int KSw = k / 16;
       bool wdone = false;
-      if (split && afm_cat_w_on() && k % 16 == 0 && KSw >= 1 && KSw <= 4) {
+      if (split && !(plan & HHFM_PLAN_PER_FIELD) && k % 16 == 0 && KSw >= 1 && KSw <= 4) {
         size_t wl = 0;
         switch (KSw) {
           case 1: wl = afm_cat_w_lds<1>(F, A); break;
@@ -1167,7 +1192,6 @@ extern "C" int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
         }
         if (wl <= 160 * 1024) {
           int64_t nch = (1024 + nq - 1) / nq;
-          if (const char* e = getenv("HHFM_AFM_W_CH")) nch = atoi(e) > 0 ? atoi(e) : nch;   // A/B
           const int64_t maxch = ntile / 32 > 1 ? ntile / 32 : 1;   // >= 4 tiles per wave
           if (nch > maxch) nch = maxch;
           const int tpw = (int)((ntile + nch - 1) / nch);

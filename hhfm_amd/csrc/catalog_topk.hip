@@ -792,128 +792,6 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
 }
 
 // ---------------------------------------------------------------------------
-// 2b. small catalogs (N <= 16,384, e.g. Frappe's 4,082 items): workgroup =
-// 16 waves = 16 queries x one item split.  Per chunk of up to 1,024 items the
-// waves score 16-item x 16-query tiles with v_mfma_f32_16x16x4_f32 (exact
-// fp32; A = item rows, lane group g taking the contiguous k-range
-// [g·k/4, (g+1)·k/4) so a lane's operand is one contiguous piece of its item
-// row; B = the queries' vectors, held in VGPRs for the whole kernel) and park
-// the 16 x 1,024 scores in LDS (one ds_write_b128 of 4 consecutive items per
-// lane and tile).  Then wave q folds query q's row of the chunk into its
-// running top-K list (topk_fold_chunk: lane-max bound, candidate compaction,
-// a bitonic sort sized to the candidates + merge).  The fold is a dependent
-// chain of cross-lane steps, so the workgroup is 16 waves (2 per CU fit:
-// 8 per SIMD) to keep the SIMDs issuing.  No [B, N] matrix touches HBM.
-// ---------------------------------------------------------------------------
-#ifndef HHFM_SMALL_KO
-#define HHFM_SMALL_KO 0   // diagnostic knock-outs: 1 = no selection, 2 = no scoring
-#endif
-constexpr int kSmallQ = 16;      // queries per workgroup (MFMA N) = waves per workgroup
-constexpr int kSmallCN = 1024;   // items per LDS chunk
-constexpr int kSmallLd = kSmallCN + 4;
-
-template <bool BF16, int KQ, int KPAD>
-__global__ __launch_bounds__(1024) void catalog_small(
-    const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
-    const char* __restrict__ E, int64_t item_row_begin, int32_t N,
-    const float* __restrict__ w, int fm, int K, int S, int items_per_split,
-    float* __restrict__ out_s, int32_t* __restrict__ out_i, int64_t ostride_b,
-    int64_t ostride_s, int32_t gbase) {
-  constexpr int k = 4 * KQ;
-  constexpr int ESZ = BF16 ? 2 : 4;
-  constexpr int NW = kSmallQ;
-  __shared__ __attribute__((aligned(16))) float sc[kSmallQ * kSmallLd];
-  __shared__ float cand_s[NW][kWave];
-  __shared__ int32_t cand_i[NW][kWave];
-
-  const int qg = blockIdx.x / S, split = blockIdx.x - (blockIdx.x / S) * S;
-  const int wv = threadIdx.x >> 6, l = lane_id();
-  const int qj = l & 15, g = l >> 4;
-  const int64_t q0 = (int64_t)qg * kSmallQ;
-
-  // B operand: query q0 + qj, k-range [g·KQ, g·KQ + KQ)  (H is zero-padded to Bpad)
-  float hq[KQ];
-  {
-    const float4* src = reinterpret_cast<const float4*>(H + (q0 + qj) * k + g * KQ);
-#pragma unroll
-    for (int v = 0; v < KQ / 4; ++v) {
-      const float4 x = src[v];
-      hq[4 * v] = x.x; hq[4 * v + 1] = x.y; hq[4 * v + 2] = x.z; hq[4 * v + 3] = x.w;
-    }
-  }
-  const float cq = fm ? cst[q0 + qj] : 0.f;
-
-  // wave wv's running list: query q0 + wv
-  float ls = kNegInf, thr = kNegInf;
-  int32_t li = kNoIdx;
-  const int32_t i0 = split * items_per_split;
-  const int32_t i1 = min(N, i0 + items_per_split);
-
-  for (int32_t cb = i0; cb < i1; cb += kSmallCN) {
-    const int cn = min(kSmallCN, i1 - cb);
-    const int ntile = (cn + 15) >> 4;
-    constexpr int NR = KQ * ESZ / 16;
-    for (int t = wv; t < ntile && !(HHFM_SMALL_KO & 2); t += NW) {
-      int item = cb + t * 16 + qj;                  // A row of this lane
-      item = item < i1 ? item : i1 - 1;
-      const uint4* row = reinterpret_cast<const uint4*>(
-          E + (item_row_begin + item) * (int64_t)(k * ESZ) + g * KQ * ESZ);
-      uint4 raw[NR];
-#pragma unroll
-      for (int v = 0; v < NR; ++v) raw[v] = row[v];
-      float av[KQ];
-#pragma unroll
-      for (int v = 0; v < NR; ++v) {
-        const uint32_t r4[4] = {raw[v].x, raw[v].y, raw[v].z, raw[v].w};
-        if constexpr (BF16) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            av[8 * v + 2 * e] = __uint_as_float(r4[e] << 16);
-            av[8 * v + 2 * e + 1] = __uint_as_float(r4[e] & 0xffff0000u);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) av[4 * v + e] = __uint_as_float(r4[e]);
-        }
-      }
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int e = 0; e < KQ; ++e)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], hq[e], acc, 0, 0, 0);
-      // acc[r] = score(item cb + 16 t + 4 g + r, query q0 + qj)
-      if (fm) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int it = cb + t * 16 + 4 * g + r;
-          const float wi = (w && it < i1) ? w[item_row_begin + it] : 0.f;
-          acc[r] = (acc[r] + wi) + cq;              // w_item, (u+f)·f   FM.py:178-184
-        }
-      }
-      *reinterpret_cast<f32x4*>(&sc[qj * kSmallLd + t * 16 + 4 * g]) = acc;
-    }
-    __syncthreads();
-    if (!(HHFM_SMALL_KO & 1)) {
-      const float* rowp = sc + wv * kSmallLd;
-      float v[kSmallCN / kWave];
-#pragma unroll
-      for (int j = 0; j < kSmallCN / kWave; ++j) {
-        const int x = j * kWave + l;
-        v[j] = x < cn ? rowp[x] : kNegInf;
-      }
-      topk_fold_chunk<KPAD, kSmallCN / kWave>(v, rowp, cb - i0, cn + (cb - i0), K, ls, li, thr,
-                                              cand_s[wv], cand_i[wv]);
-    }
-    __syncthreads();
-  }
-  // list indices are split-relative; emit global ids
-  const int64_t b = q0 + wv;
-  if (b < B && l < K) {
-    out_s[b * ostride_b + split * ostride_s + l] = ls;
-    out_i[b * ostride_b + split * ostride_s + l] = li == kNoIdx ? kNoIdx : li + i0 + gbase;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // 3. merge of R sorted lists per query
 // ---------------------------------------------------------------------------
 template <int KPAD>
@@ -987,9 +865,7 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
 struct Plan {
   int64_t Bpad;
   int nqb, S, tiles_per_split;
-  bool small;            // small catalog, k in {32, 64, 128}: catalog_small
-  int Ss, ips;           //   its item splits and items per split
-  bool dense;            // small catalog, other k: score matrix + dense top-K
+  bool dense;            // small catalog: score matrix + dense top-K
   int64_t ldsc;
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
   int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
@@ -1008,13 +884,7 @@ static bool dense_catalog(int64_t B, int32_t N) {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-static bool small_catalog(int64_t B, int32_t N, int32_t k) {
-  const char* e = getenv("HHFM_CATALOG_SMALL");
-  if (!e || e[0] != '1') return false;   // opt-in: C3 0.12 ms vs 0.096 ms on the dense path
-  return dense_catalog(B, N) && (k == 32 || k == 64 || k == 128);
-}
-
-// Threshold seed of the streaming path (default on; HHFM_CATALOG_SEED=0 off):
+// Threshold seed of the streaming path (default on; HHFM_PLAN_NO_SEED off):
 // the exact top-K of the first seed_n items (STORE score matrix + dense
 // top-K) gives every query a K-th score t before the main pass.  K catalog
 // items score >= t, so the global K-th is >= t and items below t can be
@@ -1025,12 +895,7 @@ static bool small_catalog(int64_t B, int32_t N, int32_t k) {
 // score with the same MFMA products in the same k order as the selecting
 // kernel (operands swapped: D = Aᵀ-layout), so t is bit-exactly a score the
 // main pass reproduces (tests/test_gpu_kernels.py: seeded == unseeded).
-static bool catalog_seed() {
-  const char* e = getenv("HHFM_CATALOG_SEED");
-  return !(e && e[0] == '0');
-}
-
-static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
+static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan) {
   Plan p{};
   p.nqb = (int)((B + kQPerBlock - 1) / kQPerBlock);
   p.Bpad = (int64_t)p.nqb * kQPerBlock;
@@ -1044,8 +909,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   if (S < 1) S = 1;
   p.tiles_per_split = (ntiles + S - 1) / S;
   p.S = (ntiles + p.tiles_per_split - 1) / p.tiles_per_split;
-  p.small = small_catalog(B, N, k);
-  p.dense = !p.small && dense_catalog(B, N);
+  p.dense = dense_catalog(B, N);
   for (int v = 0; v < 2; ++v) {   // catalog_ring: 2 x 4-wave or 1 x 8-wave workgroups per CU
     const int nq = 128 << v;
     p.rnqb[v] = (int)((B + nq - 1) / nq);
@@ -1054,15 +918,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
     p.rtps[v] = (ntiles + rs - 1) / rs;
     p.rS[v] = (ntiles + p.rtps[v] - 1) / p.rtps[v];
   }
-  if (p.small) {   // ~2 workgroups per CU; >= 256 items per split
-    const int nqg = (int)((B + kSmallQ - 1) / kSmallQ);
-    int ss = (512 + nqg - 1) / nqg;
-    const int smax = (N + 255) / 256;
-    ss = ss > smax ? smax : (ss < 1 ? 1 : ss);
-    p.ips = (((N + ss - 1) / ss) + 15) & ~15;
-    p.Ss = (N + p.ips - 1) / p.ips;
-  }
-  const int nsplit = p.small ? p.Ss : std::max(p.S, std::max(p.rS[0], p.rS[1]));
+  const int nsplit = std::max(p.S, std::max(p.rS[0], p.rS[1]));
   size_t off = 0;
   p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
   p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
@@ -1081,7 +937,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   // seed: up to 32,768 items and a 128 MiB score matrix, only when the
   // catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
   p.seed_n = 0;
-  if (!p.small && !p.dense && catalog_seed()) {
+  if (!p.dense && !(plan & HHFM_PLAN_NO_SEED)) {
     int64_t sn = ((int64_t)32 << 20) / p.Bpad;
     sn = (sn > HHFM_SEED_MAX ? HHFM_SEED_MAX : sn) & ~int64_t(31);
     if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
@@ -1100,28 +956,14 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K) {
   return p;
 }
 
-// HHFM_CATALOG_DENSE_GEMM=1: the small-catalog score matrix from the shared
-// LDS-tiled fp32 GEMM instead of the catalog kernel's STORE variant (A/B)
-static bool catalog_dense_gemm() {
-  const char* e = getenv("HHFM_CATALOG_DENSE_GEMM");
-  return e && e[0] == '1';
-}
-
-// HHFM_CATALOG_EXACT=1 selects the fp32-MFMA (k-ordered fmaf chain) kernel
-// instead of the split-bf16 one (A/B and numerics comparisons).
-static bool catalog_exact() {
-  const char* e = getenv("HHFM_CATALOG_EXACT");
-  return e && e[0] == '1';
-}
-
 template <bool BF16, int KT, int KPAD, bool FM>
 static void launch_main(const Plan& p, const float* H, const float* cst, int64_t B,
                         const char* E, int64_t item_row_begin, int32_t N,
                         const float* w, int K, float* os, int32_t* oi,
                         int64_t sb, int64_t ss, int32_t gbase, int32_t* gthr,
-                        hipStream_t st) {
+                        int32_t plan, hipStream_t st) {
   constexpr bool kCanSplit = BF16 || KT >= 2;   // fp32 split steps pair two chunks
-  if (kCanSplit && !catalog_exact())
+  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
     hipLaunchKernelGGL((catalog_main<BF16, KT, KPAD, FM, kCanSplit>), dim3(p.nqb * p.S),
                        dim3(256), 0, st, H, cst, B, E, item_row_begin, N, w, K,
                        p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
@@ -1131,25 +973,18 @@ static void launch_main(const Plan& p, const float* H, const float* cst, int64_t
                        p.S, p.tiles_per_split, p.nqb, os, oi, sb, ss, gbase, gthr);
 }
 
-// catalog_ring (K <= 32, bf16 k >= 128 / fp32 k >= 64, split-bf16 MFMA);
-// HHFM_CATALOG_RING=0 keeps catalog_main
-static bool catalog_ring_on() {
-  const char* e = getenv("HHFM_CATALOG_RING");
-  return !(e && e[0] == '0');
-}
-// waves per ring workgroup: HHFM_RING_WAVES=4|8 (default: 4 for bf16, 8 for fp32)
-static int ring_waves(bool bf16) {
-  const char* e = getenv("HHFM_RING_WAVES");
-  if (e && (e[0] == '4' || e[0] == '8')) return e[0] - '0';
-  return bf16 ? 4 : 8;
+// catalog_ring (K <= 32, bf16 k >= 128 / fp32 k >= 64, split-bf16 MFMA):
+// waves per workgroup 4 for bf16 tables, 8 for fp32 (HHFM_PLAN_RING_ALT swaps)
+static int ring_waves(bool bf16, int32_t plan) {
+  return (bf16 != ((plan & HHFM_PLAN_RING_ALT) != 0)) ? 4 : 8;
 }
 
 template <bool BF16, int KT, bool FM>
 static void launch_ring(const Plan& p, const float* H, const float* cst, int64_t B,
                         const char* E, int64_t item_row_begin, int32_t N, const float* w,
                         int K, float* os, int32_t* oi, int64_t sb, int64_t ss, int32_t gbase,
-                        int32_t* gthr, hipStream_t st) {
-  if (ring_waves(BF16) == 8)
+                        int32_t* gthr, int32_t plan, hipStream_t st) {
+  if (ring_waves(BF16, plan) == 8)
     hipLaunchKernelGGL((catalog_ring<BF16, KT, FM, 8>), dim3(p.rnqb[1] * p.rS[1]), dim3(512), 0,
                        st, H, cst, B, E, item_row_begin, N, w, K, p.rS[1], p.rtps[1], p.rnqb[1],
                        os, oi, sb, ss, gbase, gthr);
@@ -1163,12 +998,12 @@ template <bool BF16, bool FM>
 static bool dispatch_ring(int KT, const Plan& p, const float* H, const float* cst, int64_t B,
                           const char* E, int64_t irb, int32_t N, const float* w, int K,
                           float* os, int32_t* oi, int64_t sb, int64_t ss, int32_t gbase,
-                          int32_t* gthr, hipStream_t st) {
+                          int32_t* gthr, int32_t plan, hipStream_t st) {
   switch (KT) {
-    case 8: launch_ring<BF16, 8, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 8: launch_ring<BF16, 8, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
     case 16:
       if constexpr (BF16) return false;
-      else launch_ring<BF16, 16, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st);
+      else launch_ring<BF16, 16, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st);
       break;
     default: return false;
   }
@@ -1179,13 +1014,13 @@ template <bool BF16, int KPAD, bool FM>
 static bool dispatch_kt(int KT, const Plan& p, const float* H, const float* cst,
                         int64_t B, const char* E, int64_t irb, int32_t N,
                         const float* w, int K, float* os, int32_t* oi, int64_t sb,
-                        int64_t ss, int32_t gbase, int32_t* gthr, hipStream_t st) {
+                        int64_t ss, int32_t gbase, int32_t* gthr, int32_t plan, hipStream_t st) {
   switch (KT) {
-    case 1: launch_main<BF16, 1, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
-    case 2: launch_main<BF16, 2, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
-    case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
-    case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
-    case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, st); break;
+    case 1: launch_main<BF16, 1, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
+    case 2: launch_main<BF16, 2, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
+    case 4: launch_main<BF16, 4, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
+    case 8: launch_main<BF16, 8, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
+    case 16: launch_main<BF16, 16, KPAD, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st); break;
     default: return false;
   }
   return true;
@@ -1196,14 +1031,14 @@ static bool dispatch_kt(int KT, const Plan& p, const float* H, const float* cst,
 template <bool BF16, int KT, bool FM>
 static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const float* cst,
                          const char* E, int64_t irb, const float* w, float* sc, int64_t ldsc,
-                         int32_t* gthr, hipStream_t st) {
+                         int32_t* gthr, int32_t plan, hipStream_t st) {
   const int ntiles = (N + kTile - 1) / kTile;
   int S = (HHFM_STORE_WG + nqb - 1) / nqb;
   S = S > ntiles ? ntiles : (S < 1 ? 1 : S);
   const int tps = (ntiles + S - 1) / S;
   S = (ntiles + tps - 1) / tps;
   constexpr bool kCanSplit = BF16 || KT >= 2;
-  if (kCanSplit && !catalog_exact())
+  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
     hipLaunchKernelGGL((catalog_main<BF16, KT, 32, FM, kCanSplit, true>), dim3(nqb * S),
                        dim3(256), 0, st, H, cst, B, E, irb, N, w, 1, S, tps, nqb, sc, nullptr,
                        ldsc, 0, 0, gthr);
@@ -1216,13 +1051,13 @@ static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const fl
 template <bool BF16, bool FM>
 static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H,
                            const float* cst, const char* E, int64_t irb, const float* w,
-                           float* sc, int64_t ldsc, int32_t* gthr, hipStream_t st) {
+                           float* sc, int64_t ldsc, int32_t* gthr, int32_t plan, hipStream_t st) {
   switch (KT) {
-    case 1: launch_store<BF16, 1, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
-    case 2: launch_store<BF16, 2, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
-    case 4: launch_store<BF16, 4, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
-    case 8: launch_store<BF16, 8, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
-    case 16: launch_store<BF16, 16, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, st); break;
+    case 1: launch_store<BF16, 1, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, plan, st); break;
+    case 2: launch_store<BF16, 2, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, plan, st); break;
+    case 4: launch_store<BF16, 4, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, plan, st); break;
+    case 8: launch_store<BF16, 8, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, plan, st); break;
+    case 16: launch_store<BF16, 16, FM>(B, nqb, N, H, cst, E, irb, w, sc, ldsc, gthr, plan, st); break;
     default: return false;
   }
   return true;
@@ -1259,7 +1094,7 @@ extern "C" int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count,
                                            size_t* ws_bytes) {
   if (!ws_bytes || B < 0 || item_count < 1 || k < 1 || K < 1 || K > 64)
     return HHFM_EINVAL;
-  *ws_bytes = make_plan(B, item_count, k, K).total;
+  *ws_bytes = make_plan(B, item_count, k, K, HHFM_PLAN_DEFAULT).total;   // the largest plan
   return HHFM_OK;
 }
 
@@ -1273,7 +1108,7 @@ extern "C" int hhfm_catalog_topk(
   return hhfm_catalog_topk_ex(qidx, B, ncols, mode, user_col, ctx_begin, ctx_end, time_begin,
                               time_end, E, features_M, k, dtype, w, item_row_begin, item_count,
                               global_item_base, K, top_score, top_idx, workspace, ws_bytes,
-                              nullptr, stream);
+                              HHFM_PLAN_DEFAULT, nullptr, stream);
 }
 
 extern "C" int hhfm_catalog_topk_ex(
@@ -1282,8 +1117,9 @@ extern "C" int hhfm_catalog_topk_ex(
     int32_t time_end, const void* E, int64_t features_M, int32_t k,
     int32_t dtype, const float* w, int32_t item_row_begin, int32_t item_count,
     int32_t global_item_base, int32_t K, float* top_score, int32_t* top_idx,
-    void* workspace, size_t ws_bytes, int32_t* status, void* stream) {
+    void* workspace, size_t ws_bytes, int32_t plan, int32_t* status, void* stream) {
   if (B < 0 || ncols < 1 || ncols > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
+  if (plan & ~HHFM_PLAN_ALL) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (mode != HHFM_MODE_FM && mode != HHFM_MODE_HHFM) return HHFM_EINVAL;
   if (user_col < 0 || user_col >= ncols) return HHFM_EINVAL;
@@ -1304,7 +1140,7 @@ extern "C" int hhfm_catalog_topk_ex(
   if (!qidx || !E || !top_score || !top_idx) return HHFM_EINVAL;
   if ((reinterpret_cast<uintptr_t>(E) & 15) != 0) return HHFM_EUNSUPPORTED;
 
-  const Plan p = make_plan(B, item_count, k, K);
+  const Plan p = make_plan(B, item_count, k, K, plan);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   float* H = reinterpret_cast<float*>(ws + p.off_H);
@@ -1331,47 +1167,20 @@ extern "C" int hhfm_catalog_topk_ex(
                          ctx_end, time_begin, time_end, Eb, features_M, k, H, cst);
   }
 
-  if (p.small) {
-    const bool fmm = mode == HHFM_MODE_FM;
-    const int nqg = (int)((B + kSmallQ - 1) / kSmallQ);
-    float* os = p.Ss > 1 ? reinterpret_cast<float*>(ws + p.off_ps) : top_score;
-    int32_t* oi = p.Ss > 1 ? reinterpret_cast<int32_t*>(ws + p.off_pi) : top_idx;
-    const int64_t sb = p.Ss > 1 ? (int64_t)p.Ss * K : K, ss = p.Ss > 1 ? K : 0;
-#define HHFM_SMALL(BF, KQ, KP)                                                                \
-  hipLaunchKernelGGL((catalog_small<BF, KQ, KP>), dim3(nqg * p.Ss), dim3(1024), 0, st, H, cst, \
-                     B, Eb, (int64_t)item_row_begin, item_count, fmm ? w : nullptr, (int)fmm,  \
-                     K, p.Ss, p.ips, os, oi, sb, ss, global_item_base)
-#define HHFM_SMALL_KQ(BF, KP)                    \
-  switch (k) {                                   \
-    case 32: HHFM_SMALL(BF, 8, KP); break;       \
-    case 64: HHFM_SMALL(BF, 16, KP); break;      \
-    default: HHFM_SMALL(BF, 32, KP); break;      \
-  }
-    if (K <= 32) {
-      if (bf16) { HHFM_SMALL_KQ(true, 32) } else { HHFM_SMALL_KQ(false, 32) }
-    } else {
-      if (bf16) { HHFM_SMALL_KQ(true, 64) } else { HHFM_SMALL_KQ(false, 64) }
-    }
-#undef HHFM_SMALL_KQ
-#undef HHFM_SMALL
-    if (p.Ss > 1)
-      launch_merge(os, oi, p.Ss, B, K, /*stride_r=*/K, /*stride_b=*/(int64_t)p.Ss * K,
-                   top_score, top_idx, st);
-    return (int)hipGetLastError();
-  }
-
   if (p.dense) {
     float* sc = reinterpret_cast<float*>(ws + p.off_sc);
-    if (!catalog_dense_gemm()) {   // the score matrix from the catalog kernel (STORE)
+    const bool one = (plan & HHFM_PLAN_ONE_WAVE) != 0;
+    if (!(plan & HHFM_PLAN_GEMM)) {   // the score matrix from the catalog kernel (STORE)
       const bool fmm = mode == HHFM_MODE_FM;
       const float* wv = (fmm && w) ? w : nullptr;
       bool ok;
-      if (bf16) ok = fmm ? dispatch_store<true, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st)
-                         : dispatch_store<true, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st);
-      else ok = fmm ? dispatch_store<false, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st)
-                    : dispatch_store<false, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, st);
+      if (bf16) ok = fmm ? dispatch_store<true, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, plan, st)
+                         : dispatch_store<true, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, plan, st);
+      else ok = fmm ? dispatch_store<false, true>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, plan, st)
+                    : dispatch_store<false, false>(KT, B, p.nqb, item_count, H, cst, Eb, item_row_begin, wv, sc, p.ldsc, gthr, plan, st);
       if (ok) {
-        launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st);
+        launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st,
+                          one);
         return (int)hipGetLastError();
       }
     }
@@ -1390,20 +1199,19 @@ extern "C" int hhfm_catalog_topk_ex(
     g.C = sc;
     g.ldc = p.ldsc;
     launch_gemm(g, false, 0, st);
-    launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st);
+    launch_topk_dense(sc, B, item_count, p.ldsc, K, global_item_base, top_score, top_idx, st, one);
     return (int)hipGetLastError();
   }
 
   {   // streaming path only: the per-query threshold hints start below every
-    // score (0x80808080 decodes to ~-3.4e38); the small-catalog paths never
-    // read them
+    // score (0x80808080 decodes to ~-3.4e38); the dense path never reads them
     const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
     if (me != hipSuccess) return (int)me;
   }
   // (bf16 k = 256 would spill at two waves per SIMD: catalog_main keeps it)
   const bool ring = K <= 32 && p.seed_n > 0 && (bf16 ? KT == 8 : (KT == 8 || KT == 16)) &&
-                    !catalog_exact() && catalog_ring_on();
-  const int S_used = ring ? p.rS[ring_waves(bf16) == 8 ? 1 : 0] : p.S;
+                    !(plan & (HHFM_PLAN_EXACT_FP32 | HHFM_PLAN_NO_RING));
+  const int S_used = ring ? p.rS[ring_waves(bf16, plan) == 8 ? 1 : 0] : p.S;
   float* os;
   int32_t* oi;
   int64_t sb, ss;
@@ -1421,22 +1229,22 @@ extern "C" int hhfm_catalog_topk_ex(
   const int32_t gbase = global_item_base;  // order-preserving shift
   const bool fm = mode == HHFM_MODE_FM;
   bool ok;
-  if (p.seed_n) {   // threshold seed (catalog_seed above)
+  if (p.seed_n) {   // threshold seed (make_plan)
     float* ssc = reinterpret_cast<float*>(ws + p.off_seed_sc);
     float* sds = reinterpret_cast<float*>(ws + p.off_seed_s);
     int32_t* sdi = reinterpret_cast<int32_t*>(ws + p.off_seed_i);
     const float* wv = (fm && w) ? w : nullptr;
     const int64_t irb = item_row_begin;
-    if (bf16) ok = fm ? dispatch_store<true, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st)
-                      : dispatch_store<true, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st);
-    else ok = fm ? dispatch_store<false, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st)
-                 : dispatch_store<false, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, st);
+    if (bf16) ok = fm ? dispatch_store<true, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st)
+                      : dispatch_store<true, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st);
+    else ok = fm ? dispatch_store<false, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st)
+                 : dispatch_store<false, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st);
     if (!ok) return HHFM_EUNSUPPORTED;
     launch_topk_dense(ssc, B, p.seed_n, p.seed_n, K, 0, sds, sdi, st);
     hipLaunchKernelGGL(seed_thr_kernel, dim3((int)((B + 255) / 256)), dim3(256), 0, st, sds, B,
                        K, gthr);
   }
-#define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, st
+#define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, plan, st
   if (ring) {
     if (bf16) ok = fm ? dispatch_ring<true, true>(HHFM_MAIN_ARGS) : dispatch_ring<true, false>(HHFM_MAIN_ARGS);
     else ok = fm ? dispatch_ring<false, true>(HHFM_MAIN_ARGS) : dispatch_ring<false, false>(HHFM_MAIN_ARGS);

@@ -48,13 +48,18 @@ struct FusedDfmArgs {
   uint64_t perm;
   const int32_t* order;
   // dfm_fused_f32s: base[m] = (Σ_f w·Wp + FM part) + bp from dfm_fm_base;
-  // stage: P rows of narrow-span fields staged in LDS (HHFM_DFM_F32_STAGE=0: off)
+  // stage: P rows of narrow-span fields staged in LDS (HHFM_PLAN_UNSTAGED: off)
   const float* fmbase;
   int stage;
   // scratch for the FM part's pair table (dfm_fm_pairs); fm_out: its output
   void* scratch;
   size_t scratch_bytes;
   float* fm_out;
+  // host side only (never read by a kernel): the call's HHFM_PLAN_* flags and
+  // whether the pair table in scratch is already built for this call (the
+  // catalog's query chunks build it once)
+  int32_t plan;
+  bool* pairs_ready;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)
@@ -96,8 +101,11 @@ struct BoolC {
 // instantiated (the caller runs dfm_fused)
 bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st);
 // base[m] = (Σ_f w·Wp + FM part) + bp into a.fm_out from the pair table
-// C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip); false (nothing launched) when it does not
-// fit a.scratch or the rows are too few to pay for it
+// C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip; built once per call into a.scratch); false
+// (nothing launched) when it does not fit a.scratch, the rows are too few to
+// pay for it, or the plan asks for HHFM_PLAN_ROW_FM
 bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st);
+// split-bf16 hidden layers for the fp32 MLP (no HHFM_PLAN_EXACT_FP32)
+inline bool dfm_f32_split(int32_t plan) { return !(plan & HHFM_PLAN_EXACT_FP32); }
 
 }  // namespace hhfm

@@ -51,7 +51,6 @@
 
 namespace hhfm {
 
-bool dfm_f32_split();
 
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
 
@@ -1384,59 +1383,32 @@ __global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restri
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ Wp, float bp,
                                                          const float* __restrict__ C,
-                                                         float* __restrict__ base, int stage) {
-  __shared__ __attribute__((aligned(16))) float cst[kFmpStageB / 4];
-  __shared__ int32_t lohi[2];
-  const int tid = threadIdx.x;
-  const int64_t m = (int64_t)blockIdx.x * 256 + tid;
-  const bool live = m < B;
+                                                         float* __restrict__ base) {
+  // a row's F(F-1)/2 entries of C are gathered through L1/L2 (a block's rows
+  // share one or two users after grouping; copying their whole rows of C to
+  // LDS first measured slower)
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (m >= B) return;
   int32_t x[kFusedMaxF];
-  for (int f = 0; f < F; ++f) x[f] = live ? clamp_id(idx[m * F + f], M) : 0;
-  if (tid == 0) {
-    lohi[0] = 0x7fffffff;
-    lohi[1] = -1;
-  }
-  __syncthreads();
-  if (live) {
-    atomicMin(&lohi[0], x[0]);
-    atomicMax(&lohi[1], x[0]);
-  }
-  __syncthreads();
-  const int lo = lohi[0], span = lohi[1] - lo + 1;
-  const bool st = stage && span > 0 && (int64_t)span * M * 4 <= kFmpStageB;
-  if (st) {   // field 0's rows of C (the block's user or two)
-    const float4* src = reinterpret_cast<const float4*>(C + (int64_t)lo * M);
-    const int64_t n = (int64_t)span * M;
-    if ((M & 3) == 0) {
-      for (int64_t i = tid; i < n / 4; i += 256) reinterpret_cast<float4*>(cst)[i] = src[i];
-    } else {
-      for (int64_t i = tid; i < n; i += 256) cst[i] = C[(int64_t)lo * M + i];
-    }
-  }
-  __syncthreads();
-  if (!live) return;
+  for (int f = 0; f < F; ++f) x[f] = clamp_id(idx[m * F + f], M);
   float y2 = 0.f;
   for (int f = 0; f < F; ++f)
-    for (int g = f + 1; g < F; ++g)
-      y2 += (f == 0 && st) ? cst[(int64_t)(x[0] - lo) * M + x[g]] : C[(int64_t)x[f] * M + x[g]];
+    for (int g = f + 1; g < F; ++g) y2 += C[(int64_t)x[f] * M + x[g]];
   float y1 = 0.f;
   for (int f = 0; f < F; ++f) y1 = __fmaf_rn(w[x[f]], Wp[f], y1);
   base[m] = (y1 + y2) + bp;
-}
-
-static bool dfm_fm_pairs_on() {   // HHFM_DFM_FM_PAIRS=0: the row-reading pre-kernels
-  const char* e = getenv("HHFM_DFM_FM_PAIRS");
-  return !(e && e[0] == '0');
 }
 
 bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
   const int64_t M = a.M, B = a.B;
   const int k = a.k;
   const size_t cbytes = (size_t)M * M * 4, sbytes = (size_t)M * k * 4;
-  if (!dfm_fm_pairs_on() || !a.scratch || !a.fm_out || M > 32768 || M * 16 > B ||
-      k % 4 || cbytes + sbytes + 512 > a.scratch_bytes)
+  const bool ready = a.pairs_ready && *a.pairs_ready;
+  if ((a.plan & HHFM_PLAN_ROW_FM) || !a.scratch || !a.fm_out || M > 32768 ||
+      (!ready && M * 16 > B) || k % 4 || cbytes + sbytes + 512 > a.scratch_bytes)
     return false;
   float* Cp = reinterpret_cast<float*>(a.scratch);
+  if (!ready) {
   float* Es = reinterpret_cast<float*>(reinterpret_cast<char*>(a.scratch) +
                                        ((cbytes + 255) & ~size_t(255)));
   hipLaunchKernelGGL(dfm_scale_rows, dim3(1024), dim3(256), 0, st, a.E, (int)tbf, M, k,
@@ -1453,21 +1425,11 @@ bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
   g.C = Cp;
   g.ldc = M;
   launch_gemm(g, false, 0, st);
-  // HHFM_DFM_PAIRS_STAGE=1: a block's user rows of C staged in LDS first (the
-  // same values; copying whole rows of C per block measured slower than
-  // gathering the few entries a block reads through L1/L2)
-  static const int stage = [] {
-    const char* e = getenv("HHFM_DFM_PAIRS_STAGE");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
+  if (a.pairs_ready) *a.pairs_ready = true;
+  }
   hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
-                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out, stage);
+                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out);
   return true;
-}
-
-static bool dfm_fmb_staged() {   // HHFM_DFM_FMB_STAGE=0: the grid-stride kernel
-  const char* e = getenv("HHFM_DFM_FMB_STAGE");
-  return !(e && e[0] == '0');
 }
 
 static int fused_tm(int maxT) {
@@ -1588,32 +1550,12 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
 // proj != nullptr: the layer-0 products of fields [proj_from, F) come from
 // dfm_project_layer0's workspace (PROJ kernels; the fp32 MLP projects all
 // fields, proj_from = 0).
-// HHFM_DFM_F32_EXACT=1: the projected fp32-MLP forward keeps its hidden layers
-// on exact-fp32 MFMA (dfm_fused_f32) instead of split-bf16 (dfm_fused_f32s)
-bool dfm_f32_split() {
-  const char* e = getenv("HHFM_DFM_F32_EXACT");
-  return !(e && e[0] == '1');
-}
-// waves per workgroup of the split kernel: 8 (128 rows, default) or 4
-// (HHFM_DFM_F32_WAVES=4, 64 rows, one wave per SIMD)
-static int dfm_f32_waves() {
-  const char* e = getenv("HHFM_DFM_F32_WAVES");
-  return e && e[0] == '4' ? 4 : 8;
-}
-
-
-// HHFM_DFM_WIDE=0: the ITEM plan keeps the 128-row kernel (dfm_fused)
-static bool dfm_wide_enabled() {
-  const char* e = getenv("HHFM_DFM_WIDE");
-  return !(e && e[0] == '0');
-}
-
 bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64_t M, int k,
                       bool tbf, bool mlp_bf16, const float* w, int L, const int32_t* dims,
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
                       uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
-                      size_t scratch_bytes, hipStream_t st) {
+                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -1641,10 +1583,12 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.scratch = scratch;
   a.scratch_bytes = scratch_bytes;
   a.fm_out = fm_base;
+  a.plan = plan;
+  a.pairs_ready = pairs_ready;
   if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
     // the fp32 kernel projects all fields, in the caller's order
-    const bool split = pj && L > 1 && dfm_f32_split();
+    const bool split = pj && L > 1 && dfm_f32_split(plan);
     // (the split kernel also takes rows grouped by user: out[order[m]])
     if ((pj && proj_from != 0) || perm != kDfmIdentityPerm || (order && !split)) return false;
     const dim3 grid((unsigned)((B + kF32Rows - 1) / kF32Rows));
@@ -1673,7 +1617,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   else                                                                                     \
     hipLaunchKernelGGL((dfm_fm_base_st<false, KJ>), dim3(sblocks), dim3(256), 0, st, idx,   \
                        B, F, E, M, k, w, Wp, bp, fm_base);
-        if (dfm_fmb_staged() && kj > 0 && k * (tbf ? 2 : 4) <= kFmbStageB) {
+        if (!(plan & HHFM_PLAN_UNSTAGED) && kj > 0 && k * (tbf ? 2 : 4) <= kFmbStageB) {
           switch (kj) {
             case 1: HHFM_FMBS(1) break;
             case 2: HHFM_FMBS(2) break;
@@ -1692,25 +1636,18 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
 #undef HHFM_FMBS
       }
       a.fmbase = fm_base;
-      {
-        const char* e = getenv("HHFM_DFM_F32_STAGE");
-        a.stage = !(e && e[0] == '0');
-      }
+      a.stage = !(plan & HHFM_PLAN_UNSTAGED);
       const int64_t units = (int64_t)(L - 1) * TM * 2 * 16 * TM * 4;
       const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
       hipLaunchKernelGGL(dfm_pack_weights_f32s, dim3(pblocks), dim3(256), 0, st, a, TM,
                          reinterpret_cast<char*>(pack_ws));
-      const bool w8 = dfm_f32_waves() == 8;
+      // 8 waves x 16 rows (two waves per SIMD; one wave per SIMD measured
+      // slower)
       const dim3 g8((unsigned)((B + 127) / 128));
 #define HHFM_FUSED32S(T)                                                                   \
   case T:                                                                                  \
-    if (w8) {                                                                              \
-      if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T, 8>), g8, dim3(512), 0, st, a);   \
-      else hipLaunchKernelGGL((dfm_fused_f32s<false, T, 8>), g8, dim3(512), 0, st, a);      \
-    } else {                                                                               \
-      if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T, 4>), grid, dim3(256), 0, st, a); \
-      else hipLaunchKernelGGL((dfm_fused_f32s<false, T, 4>), grid, dim3(256), 0, st, a);    \
-    }                                                                                      \
+    if (tbf) hipLaunchKernelGGL((dfm_fused_f32s<true, T, 8>), g8, dim3(512), 0, st, a);     \
+    else hipLaunchKernelGGL((dfm_fused_f32s<false, T, 8>), g8, dim3(512), 0, st, a);        \
     break;
       switch (TM) {
         HHFM_FUSED32S(2)
@@ -1755,7 +1692,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     return true;
   }
   // the ITEM plan at an instantiated shape: 256 rows per workgroup (dfm_wide.hip)
-  if (pj && tbf && a.Fd == 1 && L == 3 && dfm_wide_enabled() && dfm_wide_launch(a, TM, st))
+  if (pj && tbf && a.Fd == 1 && L == 3 && !(plan & HHFM_PLAN_NARROW) && dfm_wide_launch(a, TM, st))
     return true;
   const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
   const int nS = a.Fd * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;

@@ -40,23 +40,7 @@ HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
 // ---------------------------------------------------------------------------
 // FM row kernel: out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0
 // ---------------------------------------------------------------------------
-// w[id] load.  WAUX < 0: plain global load (default).  WAUX >= 0: a buffer
-// load with that cache-policy operand (bit 0 sc0, bit 1 nt, bit 4 sc1) —
-// measurement variants for the 4-B `w` gathers.
-template <int WAUX>
-HHFM_DEV float load_w(const float* __restrict__ w, int32_t id, int64_t M) {
-  if constexpr (WAUX < 0) {
-    return w[id];
-  } else {
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(w), (short)0, (int)(M * 4), 0x00020000);
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, id * 4, 0, WAUX));
-  }
-}
-
-// PSTRIDE > 0: packed table, row m = [E[m] (LPR·16 B) | w[m] fp32 | pad] at a
-// row stride of PSTRIDE bytes (w read from the row, the `w` pointer unused).
-template <int F, int LPR, bool BF16, bool HAS_W, bool NT, int WAUX = -1, int PSTRIDE = 0>
+template <int F, int LPR, bool BF16, bool HAS_W, bool NT>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
     int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out,
@@ -64,7 +48,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
   constexpr int U = RowsPerLane<F>::value;
   constexpr int RPW = kWave / LPR;  // rows per wave per unroll slot
   constexpr int RPI = RPW * U;      // rows per wave-iteration
-  constexpr int64_t ROW_BYTES = PSTRIDE ? (int64_t)PSTRIDE : (int64_t)LPR * 16;
+  constexpr int64_t ROW_BYTES = (int64_t)LPR * 16;
   using C = Chunk<BF16>;
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -105,11 +89,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
           int32_t my = id[u][0];
 #pragma unroll
           for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
-          float wl;
-          if constexpr (PSTRIDE > 0)
-            wl = *reinterpret_cast<const float*>(E + (int64_t)my * PSTRIDE + LPR * 16);
-          else
-            wl = load_w<WAUX>(w, my, M);
+          const float wl = w[my];
           wv[u] += (fsel < F) ? wl : 0.f;
         }
       }
@@ -302,50 +282,6 @@ static int grid_for(int64_t rows, int64_t rows_per_block) {
   return (int)g;
 }
 
-// Measurement variants of the configs[1] shape (F=5, k=64 fp32, with w):
-// flag bits 4..7 select the cache policy of the `w` gathers.
-static bool launch_fm_wpolicy(int sel, const int32_t* idx, int64_t B, const char* E,
-                              int64_t M, const float* w, float w0, float* out,
-                              int32_t* status, hipStream_t s) {
-  constexpr int RPB = 4 * (kWave / 16) * RowsPerLane<5>::value;
-  const int grid = grid_for(B, RPB);
-#define HHFM_WPOL(SEL, AUX)                                                        \
-  case SEL:                                                                        \
-    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, AUX>), dim3(grid), \
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);         \
-    return true;
-  switch (sel) {
-    HHFM_WPOL(1, 0)
-    HHFM_WPOL(2, 1)
-    HHFM_WPOL(3, 2)
-    HHFM_WPOL(4, 3)
-    HHFM_WPOL(5, 16)
-    HHFM_WPOL(6, 17)
-    HHFM_WPOL(7, 18)
-    HHFM_WPOL(8, 19)
-    default: return false;
-  }
-#undef HHFM_WPOL
-}
-
-// Measurement variants: packed [E | w | pad] rows (flag bits 8..11: 1 = 272-B
-// stride, 2 = 384-B stride); the `w` argument is ignored, E is the packed table.
-static bool launch_fm_packed(int sel, const int32_t* idx, int64_t B, const char* E,
-                             int64_t M, float w0, float* out, int32_t* status,
-                             hipStream_t s) {
-  constexpr int RPB = 4 * (kWave / 16) * RowsPerLane<5>::value;
-  const int grid = grid_for(B, RPB);
-  if (sel == 1)
-    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, -1, 272>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, nullptr, w0, out, status);
-  else if (sel == 2)
-    hipLaunchKernelGGL((fm_rows_fast<5, 16, false, true, false, -1, 384>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, nullptr, w0, out, status);
-  else
-    return false;
-  return true;
-}
-
 template <int F, int LPR, bool BF16>
 static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            int64_t M, const float* w, float w0, float* out,
@@ -437,22 +373,13 @@ extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
                                      void* stream) {
   if (B < 0 || F < 1 || F > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
+  if (flags & ~HHFM_FLAG_STREAM_TABLE) return HHFM_EINVAL;
   if (B == 0) return HHFM_OK;
   if (!idx || !E || !out) return HHFM_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const bool bf16 = dtype == HHFM_BF16;
   const int lpr = lpr_for(k, dtype);
   const bool aligned = (reinterpret_cast<uintptr_t>(E) & 15) == 0;
-  const int wsel = (flags >> 4) & 15;
-  const int psel = (flags >> 8) & 15;
-  if (psel && F == 5 && lpr == 16 && !bf16 && aligned &&
-      launch_fm_packed(psel, idx, B, reinterpret_cast<const char*>(E), features_M, w0, out,
-                       status, s))
-    return (int)hipGetLastError();
-  if (wsel && F == 5 && lpr == 16 && !bf16 && aligned && w && features_M < (1LL << 29) &&
-      launch_fm_wpolicy(wsel, idx, B, reinterpret_cast<const char*>(E), features_M, w, w0,
-                        out, status, s))
-    return (int)hipGetLastError();
   if (!(lpr && aligned &&
         try_fm_fast(idx, B, F, reinterpret_cast<const char*>(E), features_M,
                     lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0, status,

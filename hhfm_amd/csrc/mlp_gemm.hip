@@ -31,14 +31,14 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
                       uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
-                      size_t scratch_bytes, hipStream_t st);
+                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
                         int proj_from, uint64_t perm, const void* Wt0, int N0, int L,
                         const int32_t* dims, void* ws, hipStream_t st);
 size_t dfm_order_bytes(int64_t B, int F, int64_t M);
-bool dfm_f32_split();
+inline bool dfm_f32_split(int32_t plan) { return !(plan & HHFM_PLAN_EXACT_FP32); }
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
                               void* ws, const int32_t** rows_out, hipStream_t st);
 constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
@@ -142,7 +142,7 @@ constexpr size_t kProjMaxBytes = size_t(1) << 30;
 static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dtype, int F = 0,
                         int k = 0, int64_t M = 0, int64_t rows_total = 0,
                         int proj_mode = HHFM_DFM_PROJ_OFF, int item_field = 1,
-                        bool forward = true) {
+                        bool forward = true, int32_t plan = HHFM_PLAN_DEFAULT) {
   DfmPlan p{};
   p.maxL = 0;
   for (int i = 0; i < nlayers; ++i) p.maxL = pad8(dims[i]) > p.maxL ? pad8(dims[i]) : p.maxL;
@@ -187,11 +187,10 @@ static DfmPlan dfm_plan(int64_t B, int nlayers, const int32_t* dims, int mlp_dty
       p.off_order = off;
       // fp32 MLP on the split kernel: rows grouped by user too (a block then
       // reads one or two users' P rows: L1/L2 hits instead of Infinity-Cache
-      // reads); HHFM_DFM_F32_GROUP=0 turns it off
-      const char* ge = getenv("HHFM_DFM_F32_GROUP");
-      const bool f32_group_env = !(ge && ge[0] == '0');
+      // reads); HHFM_PLAN_UNGROUPED turns it off
       const bool f32_group = !bf && mode == HHFM_DFM_PROJ_ON && forward && nlayers > 1 &&
-                             rows_total >= 64 * M && f32_group_env && dfm_f32_split();
+                             rows_total >= 64 * M && !(plan & HHFM_PLAN_UNGROUPED) &&
+                             dfm_f32_split(plan);
       if (((mode == HHFM_DFM_PROJ_ITEM) || f32_group) && forward && B <= 0x7fffffff) {
         p.group = true;
         off += al256(dfm_order_bytes(B, F, M));
@@ -236,19 +235,16 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             int32_t nlayers, const int32_t* dims, const void* const* Wt,
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
                             float bp, float* out, char* ws, const DfmPlan& p, const void* proj,
-                            const int32_t* order, hipStream_t st) {
+                            const int32_t* order, int32_t plan, bool* pairs_ready,
+                            hipStream_t st) {
   const bool bf = mlp_dtype == HHFM_BF16;
-  // One fused kernel per 128-row block when the shape fits (dfm_fused.hip,
-  // bf16 or fp32 MLP); HHFM_DFM_LAYERED=1 forces the layer-by-layer path (A/B).
-  static const bool layered = [] {
-    const char* e = getenv("HHFM_DFM_LAYERED");
-    return e && e[0] == '1';
-  }();
-  if ((proj || !layered) && p.off_proj > p.off_pack &&
+  // One fused kernel per row block when the shape fits (dfm_fused.hip /
+  // dfm_wide.hip, bf16 or fp32 MLP); the layer-by-layer GEMMs otherwise.
+  if (p.off_proj > p.off_pack &&
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
                        Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order,
                        reinterpret_cast<float*>(ws + p.off_base), ws + p.off_h0,
-                       p.off_pack - p.off_h0, st))
+                       p.off_pack - p.off_h0, plan, pairs_ready, st))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);
@@ -304,6 +300,8 @@ extern "C" int hhfm_dfm_forward_workspace(int64_t B, int32_t nlayers, const int3
   return HHFM_OK;
 }
 
+static bool plan_ok(int32_t plan) { return !(plan & ~HHFM_PLAN_ALL); }
+
 extern "C" int hhfm_dfm_forward_workspace_ex(int64_t B, int32_t F, int32_t k,
                                              int64_t features_M, int32_t nlayers,
                                              const int32_t* layer_dims, int32_t mlp_dtype,
@@ -320,7 +318,7 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
                                int32_t nlayers, const int32_t* layer_dims,
                                const void* const* Wt, const float* const* bias,
                                int32_t mlp_dtype, const float* Wp, float bp, float* out,
-                               char* ws, const DfmPlan& p, hipStream_t st) {
+                               char* ws, const DfmPlan& p, int32_t plan, hipStream_t st) {
   const void* proj = nullptr;
   const int32_t* order = nullptr;
   if (p.proj) {
@@ -335,7 +333,7 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
     if (order) idx = grouped;
   }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
-                          mlp_dtype, Wp, bp, out, ws, p, proj, order, st);
+                          mlp_dtype, Wp, bp, out, ws, p, proj, order, plan, nullptr, st);
 }
 
 static int dfm_forward_args(const int32_t* idx, int64_t B, int32_t F, const void* E,
@@ -369,7 +367,7 @@ extern "C" int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const 
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
                              bias, mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
-                             reinterpret_cast<hipStream_t>(stream));
+                             HHFM_PLAN_DEFAULT, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
@@ -377,18 +375,19 @@ extern "C" int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, con
                                    int32_t nlayers, const int32_t* layer_dims,
                                    const void* const* Wt, const float* const* bias,
                                    int32_t mlp_dtype, const float* Wp, float bp, float* out,
-                                   int32_t proj_mode, void* workspace, size_t ws_bytes,
-                                   void* stream) {
-  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
+                                   int32_t proj_mode, int32_t plan, void* workspace,
+                                   size_t ws_bytes, void* stream) {
+  if (!proj_mode_ok(proj_mode) || !plan_ok(plan)) return HHFM_EINVAL;
   const int rc = dfm_forward_args(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
                                   bias, mlp_dtype, Wp, out);
   if (rc != 1) return rc;
   if (!wt_aligned(nlayers, Wt)) proj_mode = HHFM_DFM_PROJ_OFF;
-  const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode);
+  const DfmPlan p = dfm_plan(B, nlayers, layer_dims, mlp_dtype, F, k, features_M, B, proj_mode,
+                             1, true, plan);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   return dfm_forward_planned(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
                              bias, mlp_dtype, Wp, bp, out, reinterpret_cast<char*>(workspace), p,
-                             reinterpret_cast<hipStream_t>(stream));
+                             plan, reinterpret_cast<hipStream_t>(stream));
 }
 
 // D2: chunk_rows bounds the rows (queries x items) scored per forward pass.
@@ -439,7 +438,8 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
                            const float* Wp, float bp, int32_t item_row_begin,
                            int32_t item_count, int32_t global_item_base, int32_t K,
                            int64_t chunk_rows, float* top_score, int32_t* top_idx,
-                           void* workspace, size_t ws_bytes, int proj_mode, void* stream) {
+                           void* workspace, size_t ws_bytes, int proj_mode, int32_t plan,
+                           void* stream) {
   int rc = dfm_check(B, F, k, dtype, nlayers, layer_dims, mlp_dtype);
   if (rc) return rc;
   if (item_col < 0 || item_col >= F || item_count < 1 || item_row_begin < 0 ||
@@ -460,7 +460,7 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
       p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype);
   } else {
     p = dfm_plan(rows, nlayers, layer_dims, mlp_dtype, F, k, features_M,
-                 B * (int64_t)item_count, proj_mode, item_col, false);
+                 B * (int64_t)item_count, proj_mode, item_col, false, plan);
   }
   if (!workspace || ws_bytes < dfm_cat_bytes(p, rows, F)) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
@@ -474,6 +474,9 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
                        ws + p.off_proj, st);
     proj = ws + p.off_proj;
   }
+  // the FM pair table C depends on E and Wp only: built by the first chunk,
+  // reused by the others
+  bool pairs_ready = false;
   for (int64_t b0 = 0; b0 < B; b0 += qc) {
     const int64_t nb = (B - b0) < qc ? (B - b0) : qc;
     const int64_t nrows = nb * item_count;
@@ -482,10 +485,11 @@ static int dfm_catalog_run(const int32_t* qidx, int64_t B, int32_t F, int32_t it
     hipLaunchKernelGGL(dfm_build_rows, dim3((unsigned)blocks), dim3(256), 0, st, qidx + b0 * F,
                        nb, F, item_col, item_row_begin, item_count, rbuf);
     rc = dfm_forward_impl(rbuf, nrows, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt,
-                          bias, mlp_dtype, Wp, bp, sc, ws, p, proj, nullptr, st);
+                          bias, mlp_dtype, Wp, bp, sc, ws, p, proj, nullptr, plan, &pairs_ready,
+                          st);
     if (rc) return rc;
     launch_topk_dense(sc, nb, item_count, item_count, K, global_item_base, top_score + b0 * K,
-                      top_idx + b0 * K, st);
+                      top_idx + b0 * K, st, (plan & HHFM_PLAN_ONE_WAVE) != 0);
   }
   return (int)hipGetLastError();
 }
@@ -502,7 +506,7 @@ extern "C" int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, 
   return dfm_catalog_run(qidx, B, F, item_col, E, features_M, k, dtype, w, nlayers, layer_dims,
                          Wt, bias, mlp_dtype, Wp, bp, item_row_begin, item_count,
                          global_item_base, K, chunk_rows, top_score, top_idx, workspace,
-                         ws_bytes, -1, stream);
+                         ws_bytes, -1, HHFM_PLAN_DEFAULT, stream);
 }
 
 extern "C" int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F,
@@ -514,12 +518,13 @@ extern "C" int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t 
                                         int32_t item_row_begin, int32_t item_count,
                                         int32_t global_item_base, int32_t K, int64_t chunk_rows,
                                         float* top_score, int32_t* top_idx, int32_t proj_mode,
-                                        void* workspace, size_t ws_bytes, void* stream) {
-  if (!proj_mode_ok(proj_mode)) return HHFM_EINVAL;
+                                        int32_t plan, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  if (!proj_mode_ok(proj_mode) || !plan_ok(plan)) return HHFM_EINVAL;
   return dfm_catalog_run(qidx, B, F, item_col, E, features_M, k, dtype, w, nlayers, layer_dims,
                          Wt, bias, mlp_dtype, Wp, bp, item_row_begin, item_count,
                          global_item_base, K, chunk_rows, top_score, top_idx, workspace,
-                         ws_bytes, proj_mode, stream);
+                         ws_bytes, proj_mode, plan, stream);
 }
 
 extern "C" int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,
@@ -531,5 +536,17 @@ extern "C" int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_
   if (!scores || !top_score || !top_idx) return HHFM_EINVAL;
   launch_topk_dense(scores, B, N, ld, K, global_item_base, top_score, top_idx,
                     reinterpret_cast<hipStream_t>(stream));
+  return (int)hipGetLastError();
+}
+
+extern "C" int hhfm_topk_dense_ex(const float* scores, int64_t B, int32_t N, int64_t ld,
+                                  int32_t K, int32_t global_item_base, float* top_score,
+                                  int32_t* top_idx, int32_t plan, void* stream) {
+  if (!plan_ok(plan) || B < 0 || N < 1 || ld < N || K < 1 || K > N) return HHFM_EINVAL;
+  if (K > 64) return HHFM_EUNSUPPORTED;
+  if (B == 0) return HHFM_OK;
+  if (!scores || !top_score || !top_idx) return HHFM_EINVAL;
+  launch_topk_dense(scores, B, N, ld, K, global_item_base, top_score, top_idx,
+                    reinterpret_cast<hipStream_t>(stream), (plan & HHFM_PLAN_ONE_WAVE) != 0);
   return (int)hipGetLastError();
 }

@@ -38,6 +38,17 @@ PYBIND11_MODULE(_hhfm, m) {
   m.attr("BF16") = (int)HHFM_BF16;
   m.attr("MODE_FM") = (int)HHFM_MODE_FM;
   m.attr("MODE_HHFM") = (int)HHFM_MODE_HHFM;
+  m.attr("PLAN_EXACT_FP32") = HHFM_PLAN_EXACT_FP32;
+  m.attr("PLAN_NO_SEED") = HHFM_PLAN_NO_SEED;
+  m.attr("PLAN_NO_RING") = HHFM_PLAN_NO_RING;
+  m.attr("PLAN_RING_ALT") = HHFM_PLAN_RING_ALT;
+  m.attr("PLAN_GEMM") = HHFM_PLAN_GEMM;
+  m.attr("PLAN_ROW_FM") = HHFM_PLAN_ROW_FM;
+  m.attr("PLAN_UNSTAGED") = HHFM_PLAN_UNSTAGED;
+  m.attr("PLAN_UNGROUPED") = HHFM_PLAN_UNGROUPED;
+  m.attr("PLAN_NARROW") = HHFM_PLAN_NARROW;
+  m.attr("PLAN_PER_FIELD") = HHFM_PLAN_PER_FIELD;
+  m.attr("PLAN_ONE_WAVE") = HHFM_PLAN_ONE_WAVE;
 
   m.def("abi_version", [] { return hhfm_abi_version(); });
 
@@ -95,7 +106,7 @@ PYBIND11_MODULE(_hhfm, m) {
         [](uptr qidx, int64_t B, int ncols, int mode, int ucol, int c0, int c1,
            int t0, int t1, uptr E, int64_t M, int k, int dtype, uptr w,
            int item_row_begin, int item_count, int global_item_base, int K,
-           uptr top_score, uptr top_idx, uptr ws, size_t ws_bytes, uptr status,
+           uptr top_score, uptr top_idx, uptr ws, size_t ws_bytes, int plan, uptr status,
            uptr stream) {
           int rc;
           {
@@ -104,7 +115,7 @@ PYBIND11_MODULE(_hhfm, m) {
                 P<const int32_t>(qidx), B, ncols, mode, ucol, c0, c1, t0, t1,
                 P<const void>(E), M, k, dtype, P<const float>(w),
                 item_row_begin, item_count, global_item_base, K,
-                P<float>(top_score), P<int32_t>(top_idx), P<void>(ws), ws_bytes,
+                P<float>(top_score), P<int32_t>(top_idx), P<void>(ws), ws_bytes, plan,
                 P<int32_t>(status), P<void>(stream));
           }
           check(rc, "hhfm_catalog_topk_ex");
@@ -225,7 +236,7 @@ PYBIND11_MODULE(_hhfm, m) {
   m.def("dfm_forward",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w,
            std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
-           int mlp_dtype, uptr Wp, float bp, uptr out, int proj_mode, uptr ws,
+           int mlp_dtype, uptr Wp, float bp, uptr out, int proj_mode, int plan, uptr ws,
            size_t ws_bytes, uptr stream) {
           if (Wt.size() != dims.size() || bias.size() != dims.size())
             throw py::value_error("dims, Wt and bias must have the same length");
@@ -241,7 +252,7 @@ PYBIND11_MODULE(_hhfm, m) {
             rc = hhfm_dfm_forward_ex(P<const int32_t>(idx), B, F, P<const void>(E), M, k,
                                      dtype, P<const float>(w), (int)dims.size(), dims.data(),
                                      W.data(), b.data(), mlp_dtype, P<const float>(Wp), bp,
-                                     P<float>(out), proj_mode, P<void>(ws), ws_bytes,
+                                     P<float>(out), proj_mode, plan, P<void>(ws), ws_bytes,
                                      P<void>(stream));
           }
           check(rc, "hhfm_dfm_forward_ex");
@@ -273,7 +284,7 @@ PYBIND11_MODULE(_hhfm, m) {
            uptr w, std::vector<int32_t> dims, std::vector<uptr> Wt, std::vector<uptr> bias,
            int mlp_dtype, uptr Wp, float bp, int item_row_begin, int item_count,
            int global_item_base, int K, int64_t chunk_rows, uptr top_score, uptr top_idx,
-           int proj_mode, uptr ws, size_t ws_bytes, uptr stream) {
+           int proj_mode, int plan, uptr ws, size_t ws_bytes, uptr stream) {
           if (Wt.size() != dims.size() || bias.size() != dims.size())
             throw py::value_error("dims, Wt and bias must have the same length");
           std::vector<const void*> W(Wt.size());
@@ -291,7 +302,7 @@ PYBIND11_MODULE(_hhfm, m) {
                                           mlp_dtype, P<const float>(Wp), bp, item_row_begin,
                                           item_count, global_item_base, K, chunk_rows,
                                           P<float>(top_score), P<int32_t>(top_idx), proj_mode,
-                                          P<void>(ws), ws_bytes, P<void>(stream));
+                                          plan, P<void>(ws), ws_bytes, P<void>(stream));
           }
           check(rc, "hhfm_dfm_catalog_topk_ex");
         });
@@ -304,43 +315,44 @@ PYBIND11_MODULE(_hhfm, m) {
 
   m.def("afm_forward",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w, float w0,
-           uptr Wt, uptr ab, uptr ap, int A, uptr P, uptr out, uptr ws, size_t ws_bytes,
-           uptr stream) {
+           uptr Wt, uptr ab, uptr ap, int A, uptr P, uptr out, int plan, uptr ws,
+           size_t ws_bytes, uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_afm_forward(P_<const int32_t>(idx), B, F, P_<const void>(E), M, k, dtype,
-                                  P_<const float>(w), w0, P_<const float>(Wt),
-                                  P_<const float>(ab), P_<const float>(ap), A,
-                                  P_<const float>(P), P_<float>(out), P_<void>(ws), ws_bytes,
-                                  P_<void>(stream));
+            rc = hhfm_afm_forward_ex(P_<const int32_t>(idx), B, F, P_<const void>(E), M, k,
+                                     dtype, P_<const float>(w), w0, P_<const float>(Wt),
+                                     P_<const float>(ab), P_<const float>(ap), A,
+                                     P_<const float>(P), P_<float>(out), plan, P_<void>(ws),
+                                     ws_bytes, P_<void>(stream));
           }
-          check(rc, "hhfm_afm_forward");
+          check(rc, "hhfm_afm_forward_ex");
         });
 
   m.def("afm_catalog_topk_workspace",
-        [](int64_t B, int F, int k, int A, int item_count, int64_t max_cols) {
+        [](int64_t B, int F, int k, int A, int item_count, int64_t max_cols, int plan) {
           size_t ws = 0;
-          check(hhfm_afm_catalog_topk_workspace(B, F, k, A, item_count, max_cols, &ws),
-                "hhfm_afm_catalog_topk_workspace");
+          check(hhfm_afm_catalog_topk_workspace_ex(B, F, k, A, item_count, max_cols, plan, &ws),
+                "hhfm_afm_catalog_topk_workspace_ex");
           return ws;
         });
 
   m.def("afm_catalog_topk",
         [](uptr q, int64_t B, int F, uptr E, int64_t M, int k, int dtype, uptr w, uptr Wt,
            uptr ab, uptr ap, int A, uptr P, int irb, int cnt, int gbase, int K,
-           int64_t max_cols, uptr ts, uptr ti, uptr ws, size_t ws_bytes, uptr stream) {
+           int64_t max_cols, uptr ts, uptr ti, int plan, uptr ws, size_t ws_bytes,
+           uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_afm_catalog_topk(P_<const int32_t>(q), B, F, P_<const void>(E), M, k,
-                                       dtype, P_<const float>(w), P_<const float>(Wt),
-                                       P_<const float>(ab), P_<const float>(ap), A,
-                                       P_<const float>(P), irb, cnt, gbase, K, max_cols,
-                                       P_<float>(ts), P_<int32_t>(ti), P_<void>(ws), ws_bytes,
-                                       P_<void>(stream));
+            rc = hhfm_afm_catalog_topk_ex(P_<const int32_t>(q), B, F, P_<const void>(E), M, k,
+                                          dtype, P_<const float>(w), P_<const float>(Wt),
+                                          P_<const float>(ab), P_<const float>(ap), A,
+                                          P_<const float>(P), irb, cnt, gbase, K, max_cols,
+                                          P_<float>(ts), P_<int32_t>(ti), plan, P_<void>(ws),
+                                          ws_bytes, P_<void>(stream));
           }
-          check(rc, "hhfm_afm_catalog_topk");
+          check(rc, "hhfm_afm_catalog_topk_ex");
         });
 
   m.def("train_workspace", [](int64_t M, int k) { return hhfm_train_workspace(M, k); });
@@ -438,14 +450,15 @@ PYBIND11_MODULE(_hhfm, m) {
 
   m.def("topk_dense",
         [](uptr scores, int64_t B, int N, int64_t ld, int K, int base, uptr top_score,
-           uptr top_idx, uptr stream) {
+           uptr top_idx, int plan, uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
-            rc = hhfm_topk_dense(P<const float>(scores), B, N, ld, K, base, P<float>(top_score),
-                                 P<int32_t>(top_idx), P<void>(stream));
+            rc = hhfm_topk_dense_ex(P<const float>(scores), B, N, ld, K, base,
+                                    P<float>(top_score), P<int32_t>(top_idx), plan,
+                                    P<void>(stream));
           }
-          check(rc, "hhfm_topk_dense");
+          check(rc, "hhfm_topk_dense_ex");
         });
 
   m.def("topk_merge_host",

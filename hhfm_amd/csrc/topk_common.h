@@ -287,18 +287,19 @@ __global__ __launch_bounds__(256) void topk_dense_split_kernel(const float* __re
   }
 }
 
-// HHFM_TOPK_WPQ=1 keeps one wave per query at every B (A/B)
-static inline int topk_dense_wpq(int64_t B, int32_t N) {
-  const char* e = getenv("HHFM_TOPK_WPQ");
-  if (e && e[0] == '1') return 1;
-  if (N < 1024) return 1;
+// waves per query: 4 for <= 1,024 queries of >= 1,024 items (each folds a
+// 64-aligned quarter, the first merges); one_wave (HHFM_PLAN_ONE_WAVE) keeps
+// one wave per query at every size
+static inline int topk_dense_wpq(int64_t B, int32_t N, bool one_wave) {
+  if (one_wave || N < 1024) return 1;
   // (2 waves per query at 3,000 queries measured 48.4 vs 46.2 µs for C3)
   return B <= 1024 ? 4 : 1;
 }
 
 static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds, int K,
-                              int32_t base, float* os, int32_t* oi, hipStream_t st) {
-  const int wpq = topk_dense_wpq(B, N);
+                              int32_t base, float* os, int32_t* oi, hipStream_t st,
+                              bool one_wave = false) {
+  const int wpq = topk_dense_wpq(B, N, one_wave);
   if (wpq > 1) {
     const int qb = 4 / wpq;
     int64_t blocks = (B + qb - 1) / qb;

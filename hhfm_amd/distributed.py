@@ -46,20 +46,28 @@ def _pad(scores: torch.Tensor, ids: torch.Tensor, K: int):
     return ps, pi
 
 
+def comm_device(group=None) -> torch.device:
+    """Where this rank's collective payloads live: its GPU for RCCL
+    (backend ``nccl``), host memory for gloo (the CPU tests).  The
+    collective calls themselves are the same for every backend."""
+    if dist.is_initialized() and dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def gather_topk(scores: torch.Tensor, ids: torch.Tensor, group=None):
     """All-gather each rank's [B,K] lists -> [R,B,K] (rank-major).
 
     One collective: (score bits, id) are packed as an int32 [B,K,2] payload
-    (8 B per entry), so the latency-bound exchange is a single RCCL
-    all-gather instead of one per field."""
+    (8 B per entry), so the latency-bound exchange is a single all-gather
+    into one dim-0-concatenated [R·B, K, 2] tensor — the same call for RCCL
+    and for gloo, so the gloo tests run exactly the code path RCCL runs."""
     world = dist.get_world_size(group)
     B, K = scores.shape
     packed = torch.stack([scores.contiguous().view(torch.int32), ids.contiguous()], dim=2)
-    out = torch.empty(world, B, K, 2, dtype=torch.int32, device=packed.device)
-    if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, packed, group=group)
-    else:
-        dist.all_gather(list(out.unbind(0)), packed, group=group)
+    out = torch.empty(world * B, K, 2, dtype=torch.int32, device=packed.device)
+    dist.all_gather_into_tensor(out, packed, group=group)
+    out = out.view(world, B, K, 2)
     return out[..., 0].contiguous().view(torch.float32), out[..., 1].contiguous()
 
 
@@ -84,8 +92,7 @@ def sharded_topk(A, K: int, n_item: int, local_scorer: LocalScorer, group=None):
         s, i = _pad(s, i, K)
     else:
         B = len(A)
-        dev = torch.device("cuda", torch.cuda.current_device()) if \
-            dist.is_initialized() and dist.get_backend(group) == "nccl" else torch.device("cpu")
+        dev = comm_device(group)
         s = torch.full((B, K), NEG_INF, dtype=torch.float32, device=dev)
         i = torch.full((B, K), NO_IDX, dtype=torch.int32, device=dev)
     if world == 1:
@@ -152,10 +159,7 @@ def sharded_evaluate_auc(tr, data1, group=None) -> float:
             total += pos_score.size
         if tr.auc_first_chunk_only:
             break
-    t = torch.tensor([hits, total], dtype=torch.float64)
+    t = torch.tensor([hits, total], dtype=torch.float64, device=comm_device(group))
     if world > 1:
-        backend = dist.get_backend(group)
-        if backend == "nccl":
-            t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return float(t[0] / t[1])

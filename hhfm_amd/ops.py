@@ -15,6 +15,22 @@ from ._native import native
 MODE_FM = 0
 MODE_HHFM = 1
 
+# Plan flags (include/hhfm.h, ABI v4): explicit per-call kernel choices; 0 is
+# the default plan.  PLAN_EXACT_FP32 selects k-ordered fp32-MFMA arithmetic
+# instead of split-bf16; the others force a fallback kernel on the same
+# scores (tests compare both paths on one shape).
+PLAN_EXACT_FP32 = 1 << 0
+PLAN_NO_SEED = 1 << 1
+PLAN_NO_RING = 1 << 2
+PLAN_RING_ALT = 1 << 3
+PLAN_GEMM = 1 << 4
+PLAN_ROW_FM = 1 << 5
+PLAN_UNSTAGED = 1 << 6
+PLAN_UNGROUPED = 1 << 7
+PLAN_NARROW = 1 << 8
+PLAN_PER_FIELD = 1 << 9
+PLAN_ONE_WAVE = 1 << 10
+
 
 def _dtype_code(t: torch.Tensor) -> int:
     if t.dtype == torch.float32:
@@ -145,10 +161,12 @@ def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
                  item_row_begin: int, item_count: int, global_item_base: int = 0,
                  w: Optional[torch.Tensor] = None, user_col: int = 0,
                  ctx: Tuple[int, int] = (0, 0), time: Tuple[int, int] = (0, 0),
-                 status: Optional[torch.Tensor] = None
+                 status: Optional[torch.Tensor] = None, plan: int = 0
                  ) -> Tuple[torch.Tensor, torch.Tensor]:
     """Full-catalog score + top-K (FM.topk FM.py:172-198, OUR.topk
-    OurModel7.py:229-307). Returns (scores float32 [B,K], ids int32 [B,K])."""
+    OurModel7.py:229-307). Returns (scores float32 [B,K], ids int32 [B,K]).
+    ``plan``: PLAN_* flags (PLAN_EXACT_FP32, _NO_SEED, _NO_RING, _RING_ALT,
+    _GEMM, _ONE_WAVE)."""
     _idx(qidx, "qidx")
     dev = _need_cuda(qidx, E, w)
     B, ncols = qidx.shape
@@ -162,7 +180,7 @@ def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
                      time[0], time[1], E.data_ptr(), M, k, _dtype_code(E),
                      0 if w is None else w.data_ptr(), item_row_begin, item_count,
                      global_item_base, K, top_s.data_ptr(), top_i.data_ptr(),
-                     ws.data_ptr(), ws.numel(), _status_ptr(status), _stream(dev))
+                     ws.data_ptr(), ws.numel(), int(plan), _status_ptr(status), _stream(dev))
     return top_s, top_i
 
 
@@ -222,13 +240,14 @@ DFM_PROJ = {False: 0, True: 1, None: 2, "ctx": 3, "item": 4}
 def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                 mlp_dtype: torch.dtype, Wp: torch.Tensor, bp: float,
                 out: Optional[torch.Tensor] = None,
-                proj=None) -> torch.Tensor:
+                proj=None, plan: int = 0) -> torch.Tensor:
     """DeepFM.out (DFM.py:104-137) for rows ``idx`` [B, F] -> float32 [B].
 
     ``proj``: projected layer 0 (include/hhfm.h, ABI v3) — None lets the
     library decide (include/hhfm.h HHFM_DFM_PROJ_AUTO), True / False force it
     on / off, "ctx" projects the context fields 2..F-1 only and "item" every
-    field but the item (bf16 MLP)."""
+    field but the item (bf16 MLP).  ``plan``: PLAN_* flags (fp32 MLP:
+    PLAN_EXACT_FP32, _ROW_FM, _UNSTAGED, _UNGROUPED; bf16 MLP: _NARROW)."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, Wp, *Wt, *bias)
     B, F = idx.shape
@@ -243,17 +262,17 @@ def dfm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, d
     ws = _workspace(dev, nbytes)
     nat.dfm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
                     list(dims), [t.data_ptr() for t in Wt], [t.data_ptr() for t in bias], md,
-                    Wp.data_ptr(), float(bp), out.data_ptr(), DFM_PROJ[proj], ws.data_ptr(),
-                    ws.numel(), _stream(dev))
+                    Wp.data_ptr(), float(bp), out.data_ptr(), DFM_PROJ[proj], int(plan),
+                    ws.data_ptr(), ws.numel(), _stream(dev))
     return out
 
 
 def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, bias, dims,
                      Wp: torch.Tensor, bp: float, item_col: int, item_row_begin: int,
                      item_count: int, K: int, global_item_base: int = 0,
-                     chunk_rows: int = 1 << 20, proj=None):
-    """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K]); ``proj`` as
-    in :func:`dfm_forward` (rows = B x item_count)."""
+                     chunk_rows: int = 1 << 20, proj=None, plan: int = 0):
+    """DeepFM.topk (DFM.py:219-231) -> (scores [B,K], ids [B,K]); ``proj`` and
+    ``plan`` as in :func:`dfm_forward` (rows = B x item_count)."""
     _idx(qidx, "qidx")
     dev = _need_cuda(qidx, E, w, Wp, *Wt, *bias)
     B, F = qidx.shape
@@ -269,13 +288,14 @@ def dfm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt, b
                          w.data_ptr(), list(dims), [t.data_ptr() for t in Wt],
                          [t.data_ptr() for t in bias], md, Wp.data_ptr(), float(bp),
                          item_row_begin, item_count, global_item_base, K, chunk_rows,
-                         top_s.data_ptr(), top_i.data_ptr(), DFM_PROJ[proj], ws.data_ptr(),
-                         ws.numel(), _stream(dev))
+                         top_s.data_ptr(), top_i.data_ptr(), DFM_PROJ[proj], int(plan),
+                         ws.data_ptr(), ws.numel(), _stream(dev))
     return top_s, top_i
 
 
-def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0):
-    """tf.nn.top_k over a device score matrix [B, N] (K <= 64)."""
+def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0, plan: int = 0):
+    """tf.nn.top_k over a device score matrix [B, N] (K <= 64); ``plan``
+    PLAN_ONE_WAVE keeps one wave per query."""
     _need_cuda(scores)
     if scores.dtype != torch.float32 or scores.dim() != 2:
         raise TypeError("scores must be float32 [B, N]")
@@ -283,7 +303,7 @@ def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0):
     top_s = torch.empty(B, K, dtype=torch.float32, device=scores.device)
     top_i = torch.empty(B, K, dtype=torch.int32, device=scores.device)
     native().topk_dense(scores.data_ptr(), B, N, scores.stride(0), K, global_item_base,
-                        top_s.data_ptr(), top_i.data_ptr(), _stream(scores.device))
+                        top_s.data_ptr(), top_i.data_ptr(), int(plan), _stream(scores.device))
     return top_s, top_i
 
 
@@ -292,9 +312,10 @@ def topk_dense(scores: torch.Tensor, K: int, global_item_base: int = 0):
 # ---------------------------------------------------------------------------
 def afm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, w0: float,
                 Wt: torch.Tensor, att_b: torch.Tensor, att_p: torch.Tensor, P: torch.Tensor,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                out: Optional[torch.Tensor] = None, plan: int = 0) -> torch.Tensor:
     """AFM.out (AFM.py:103-142) for rows ``idx`` [B, F] -> float32 [B].
-    ``Wt`` is attention_W transposed, [A, k] float32."""
+    ``Wt`` is attention_W transposed, [A, k] float32; ``plan`` PLAN_EXACT_FP32
+    keeps the contraction on exact-fp32 MFMA."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, Wt, att_b, att_p, P)
     B, F = idx.shape
@@ -306,28 +327,30 @@ def afm_forward(idx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, w0: float,
     ws = _workspace(dev, nat.afm_forward_workspace(B, F, A))
     nat.afm_forward(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
                     float(w0), Wt.data_ptr(), att_b.data_ptr(), att_p.data_ptr(), A, P.data_ptr(),
-                    out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(dev))
+                    out.data_ptr(), int(plan), ws.data_ptr(), ws.numel(), _stream(dev))
     return out
 
 
 def afm_catalog_topk(qidx: torch.Tensor, E: torch.Tensor, w: torch.Tensor, Wt: torch.Tensor,
                      att_b: torch.Tensor, att_p: torch.Tensor, P: torch.Tensor,
                      item_row_begin: int, item_count: int, K: int, global_item_base: int = 0,
-                     max_cols: int = 1 << 17):
-    """AFM.topk (AFM.py:209-246) -> (scores [B,K], ids [B,K])."""
+                     max_cols: int = 1 << 17, plan: int = 0):
+    """AFM.topk (AFM.py:209-246) -> (scores [B,K], ids [B,K]); ``plan``:
+    PLAN_EXACT_FP32, _PER_FIELD, _GEMM."""
     _idx(qidx, "qidx")
     dev = _need_cuda(qidx, E, w, Wt, att_b, att_p, P)
     B, F = qidx.shape
     M, k = E.shape
     A = Wt.shape[0]
     nat = native()
-    ws = _workspace(dev, nat.afm_catalog_topk_workspace(B, F, k, A, item_count, max_cols))
+    ws = _workspace(dev, nat.afm_catalog_topk_workspace(B, F, k, A, item_count, max_cols,
+                                                        int(plan)))
     top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
     top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
     nat.afm_catalog_topk(qidx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E), w.data_ptr(),
                          Wt.data_ptr(), att_b.data_ptr(), att_p.data_ptr(), A, P.data_ptr(),
                          item_row_begin, item_count, global_item_base, K, max_cols,
-                         top_s.data_ptr(), top_i.data_ptr(), ws.data_ptr(), ws.numel(),
+                         top_s.data_ptr(), top_i.data_ptr(), int(plan), ws.data_ptr(), ws.numel(),
                          _stream(dev))
     return top_s, top_i
 

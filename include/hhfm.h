@@ -30,9 +30,38 @@
 extern "C" {
 #endif
 
-#define HHFM_ABI_VERSION 3
+#define HHFM_ABI_VERSION 4
 
 enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
+
+/* Plan flags (ABI v4).  Which kernel runs is chosen from the shapes and these
+ * per-call flags only — the library reads no environment variable.  0 is the
+ * default plan.  HHFM_PLAN_EXACT_FP32 is the one NUMERICS choice: the dot
+ * products run as k-ordered fp32 fmaf chains on fp32 MFMA instead of on bf16
+ * MFMA over an exact three-piece bf16 split of every fp32 operand (both within
+ * 1e-5 relative of the reference).  Every other bit forces an
+ * alternative kernel that other shapes take anyway (same products; bit-
+ * identical, or the same terms summed in another order) so the tests can
+ * compare both paths on one shape.  Bits an entry point does not use are
+ * ignored; bits outside HHFM_PLAN_ALL are rejected with HHFM_EINVAL. */
+#define HHFM_PLAN_DEFAULT 0
+#define HHFM_PLAN_EXACT_FP32 (1 << 0) /* catalog, AFM, DeepFM fp32 hidden layers */
+#define HHFM_PLAN_NO_SEED (1 << 1)    /* catalog streaming path: no threshold-seed pass */
+#define HHFM_PLAN_NO_RING (1 << 2)    /* catalog streaming path: catalog_main, not the ring */
+#define HHFM_PLAN_RING_ALT (1 << 3)   /* catalog ring: 8 waves per workgroup for bf16
+                                         tables, 4 for fp32 (default: the other way) */
+#define HHFM_PLAN_GEMM (1 << 4)       /* small catalog and AFM catalog: the score matrix
+                                         from the shared LDS-tiled fp32 GEMM */
+#define HHFM_PLAN_ROW_FM (1 << 5)     /* DeepFM fp32 MLP: FM part from the table rows,
+                                         not from the pair table C = (E*Wp)E^T */
+#define HHFM_PLAN_UNSTAGED (1 << 6)   /* DeepFM fp32 MLP: P rows and table rows read
+                                         through the caches, not staged in LDS */
+#define HHFM_PLAN_UNGROUPED (1 << 7)  /* DeepFM fp32 MLP: rows not grouped by user */
+#define HHFM_PLAN_NARROW (1 << 8)     /* DeepFM bf16 ITEM plan: 128-row kernel, not 192 */
+#define HHFM_PLAN_PER_FIELD (1 << 9)  /* AFM catalog: pair product split per query field
+                                         (afm_cat_fused), not the folded weights */
+#define HHFM_PLAN_ONE_WAVE (1 << 10)  /* dense top-K: one wave per query at every size */
+#define HHFM_PLAN_ALL ((1 << 11) - 1)
 
 /* catalog scoring modes */
 enum hhfm_catalog_mode {
@@ -63,10 +92,8 @@ int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
 
 /* Same, with tuning flags and an optional id status word:
  *   HHFM_FLAG_STREAM_TABLE — read embedding rows / ids and write `out` with
- *   non-temporal accesses, so the small, re-read bias table w stays resident
- *   in L2 / the 256 MB Infinity Cache while the (huge) table streams past.
- *   Bits 4..7 select measurement variants of the `w` gather's cache policy
- *   (F=5, k=64 fp32 only; scripts/k1_wpolicy.py).
+ *   non-temporal accesses (measured 10 % slower at configs[1]).
+ *   Any other bit is rejected with HHFM_EINVAL.
  * status: NULL, or a device int32 the kernel ORs HHFM_STATUS_BAD_ID into when
  *   it meets an id outside [0, features_M) (such ids are read as row 0 so the
  *   kernel cannot fault).  hhfm_status_read() turns it into HHFM_EINVAL —
@@ -118,9 +145,10 @@ int hhfm_hybrid_score_rows_ex(const int32_t* idx, int64_t B, int32_t ncols,
  *   arithmetic: the h·item products run on bf16 MFMA with every fp32
  *            operand split exactly into three bf16 pieces (products of
  *            order >= 2^-16 kept, fp32 accumulation: ~1e-7 relative to a
- *            k-ordered fp32 chain); HHFM_CATALOG_EXACT=1 in the environment
+ *            k-ordered fp32 chain); plan HHFM_PLAN_EXACT_FP32 (the _ex form)
  *            selects the fp32-MFMA kernels (the k-ordered fmaf chain).
- * Workspace: query `hhfm_catalog_topk_workspace` with the same sizes.
+ * Workspace: query `hhfm_catalog_topk_workspace` with the same sizes (it
+ * covers every plan).
  * ---------------------------------------------------------------------- */
 int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count, int32_t k,
                                 int32_t K, size_t* ws_bytes);
@@ -133,8 +161,9 @@ int hhfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t ncols,
                       int32_t item_count, int32_t global_item_base, int32_t K,
                       float* top_score, int32_t* top_idx, void* workspace,
                       size_t ws_bytes, void* stream);
-/* Same, with the optional id status word (query ids are checked on the
- * stream before scoring; the item range is checked on the host). */
+/* Same, with plan flags (HHFM_PLAN_EXACT_FP32, _NO_SEED, _NO_RING,
+ * _RING_ALT, _GEMM, _ONE_WAVE) and the optional id status word (query ids
+ * are checked on the stream before scoring; the item range on the host). */
 int hhfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t ncols,
                          int32_t mode, int32_t user_col, int32_t ctx_begin,
                          int32_t ctx_end, int32_t time_begin, int32_t time_end,
@@ -142,7 +171,7 @@ int hhfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t ncols,
                          int32_t dtype, const float* w, int32_t item_row_begin,
                          int32_t item_count, int32_t global_item_base, int32_t K,
                          float* top_score, int32_t* top_idx, void* workspace,
-                         size_t ws_bytes, int32_t* status, void* stream);
+                         size_t ws_bytes, int32_t plan, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * Top-K merge of R sorted partial lists per query (the item-sharded
@@ -220,14 +249,16 @@ int hhfm_dfm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
                      const float* const* bias, int32_t mlp_dtype, const float* Wp,
                      float bp, float* out, void* workspace, size_t ws_bytes,
                      void* stream);
-/* Same, with the projection mode explicit; ws_bytes must cover
- * hhfm_dfm_forward_workspace_ex(..., proj_mode). */
+/* Same, with the projection mode and the plan flags explicit (fp32 MLP:
+ * HHFM_PLAN_EXACT_FP32 keeps the hidden layers on exact-fp32 MFMA, _ROW_FM,
+ * _UNSTAGED, _UNGROUPED; bf16 MLP: _NARROW; the catalog also _ONE_WAVE);
+ * ws_bytes must cover hhfm_dfm_forward_workspace_ex(..., proj_mode). */
 int hhfm_dfm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
                         int64_t features_M, int32_t k, int32_t dtype, const float* w,
                         int32_t nlayers, const int32_t* layer_dims, const void* const* Wt,
                         const float* const* bias, int32_t mlp_dtype, const float* Wp,
-                        float bp, float* out, int32_t proj_mode, void* workspace,
-                        size_t ws_bytes, void* stream);
+                        float bp, float* out, int32_t proj_mode, int32_t plan,
+                        void* workspace, size_t ws_bytes, void* stream);
 
 /* D2 — DeepFM.topk (DFM.py:219-231): every query row is tiled over the
  * catalog with column item_col replaced by each item id, scored by D1 and
@@ -250,7 +281,8 @@ int hhfm_dfm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, int32_t ite
                           int32_t global_item_base, int32_t K, int64_t chunk_rows,
                           float* top_score, int32_t* top_idx, void* workspace,
                           size_t ws_bytes, void* stream);
-/* Same, with the projection mode explicit (see hhfm_dfm_forward_ex). */
+/* Same, with the projection mode and plan flags explicit (see
+ * hhfm_dfm_forward_ex). */
 int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, int32_t item_col,
                              const void* E, int64_t features_M, int32_t k, int32_t dtype,
                              const float* w, int32_t nlayers, const int32_t* layer_dims,
@@ -259,7 +291,7 @@ int hhfm_dfm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, int32_t 
                              int32_t item_row_begin, int32_t item_count,
                              int32_t global_item_base, int32_t K, int64_t chunk_rows,
                              float* top_score, int32_t* top_idx, int32_t proj_mode,
-                             void* workspace, size_t ws_bytes, void* stream);
+                             int32_t plan, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * A1 — AFM per-row score (replaces `AFM.out`, AFM.py:103-142), attention on,
@@ -274,6 +306,13 @@ int hhfm_afm_forward(const int32_t* idx, int64_t B, int32_t F, const void* E,
                      const float* Wt, const float* att_b, const float* att_p, int32_t A,
                      const float* P, float* out, void* workspace, size_t ws_bytes,
                      void* stream);
+/* Same, with plan flags: HHFM_PLAN_EXACT_FP32 runs the attention contraction
+ * on exact-fp32 MFMA instead of split-bf16 (k % 16 == 0 shapes). */
+int hhfm_afm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
+                        int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                        float w0, const float* Wt, const float* att_b, const float* att_p,
+                        int32_t A, const float* P, float* out, int32_t plan,
+                        void* workspace, size_t ws_bytes, void* stream);
 
 /* A2 — AFM.topk (AFM.py:209-246): uf = [E[col 0], E[cols 2..F-1]], exp-weighted
  * pair attention over uf pairs and uf x item pairs (raw exp, as the
@@ -290,6 +329,18 @@ int hhfm_afm_catalog_topk(const int32_t* qidx, int64_t B, int32_t F, const void*
                           int32_t item_count, int32_t global_item_base, int32_t K,
                           int64_t max_cols, float* top_score, int32_t* top_idx,
                           void* workspace, size_t ws_bytes, void* stream);
+/* Same, with plan flags: HHFM_PLAN_EXACT_FP32, _PER_FIELD, _GEMM (the
+ * workspace for _GEMM is hhfm_afm_catalog_topk_workspace_ex's). */
+int hhfm_afm_catalog_topk_workspace_ex(int64_t B, int32_t F, int32_t k, int32_t A,
+                                       int32_t item_count, int64_t max_cols, int32_t plan,
+                                       size_t* ws_bytes);
+int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, const void* E,
+                             int64_t features_M, int32_t k, int32_t dtype, const float* w,
+                             const float* Wt, const float* att_b, const float* att_p,
+                             int32_t A, const float* P, int32_t item_row_begin,
+                             int32_t item_count, int32_t global_item_base, int32_t K,
+                             int64_t max_cols, float* top_score, int32_t* top_idx,
+                             int32_t plan, void* workspace, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * H6 — one training step (`partial_fit`, sess.run((loss, optimizer))).
@@ -358,6 +409,11 @@ int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F
 int hhfm_topk_dense(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,
                     int32_t global_item_base, float* top_score, int32_t* top_idx,
                     void* stream);
+/* Same, with plan flags: HHFM_PLAN_ONE_WAVE keeps one wave per query where
+ * the default splits a query over 4 waves (B <= 1,024, N >= 1,024). */
+int hhfm_topk_dense_ex(const float* scores, int64_t B, int32_t N, int64_t ld, int32_t K,
+                       int32_t global_item_base, float* top_score, int32_t* top_idx,
+                       int32_t plan, void* stream);
 
 /* ------------------------------------------------------------------------
  * H5 / H3 — harness membership test and metric walk

@@ -152,6 +152,21 @@ def dfm_magnitude(X, E, w, layers, biases, Wp, bp):
     return (np.abs(cat * Wp.reshape(1, -1))).sum(1) + abs(float(bp))
 
 
+def dfm_rows_exact(X, E, w, layers, biases, Wp, bp):
+    """float64 DeepFM.out of DFM.py:104-137 (ReLU after every layer, :128) and
+    its natural magnitude Σ_j |concat_j · Wp_j| + |bp| per row."""
+    X = np.asarray(X, np.int64)
+    e = np.asarray(E, np.float64)[X]
+    y1 = np.asarray(w, np.float64).reshape(-1)[X]
+    s = e.sum(1)
+    y2 = 0.5 * (s * s - (e * e).sum(1))
+    h = e.reshape(len(X), -1)
+    for Wl, bl in zip(layers, biases):
+        h = np.maximum(h @ np.asarray(Wl, np.float64) + np.asarray(bl, np.float64).reshape(-1), 0)
+    t = np.concatenate([y1, y2, h], 1) * np.asarray(Wp, np.float64).reshape(1, -1)
+    return t.sum(1) + float(bp), np.abs(t).sum(1) + abs(float(bp))
+
+
 def dfm_bf16_out(X, E, w, layers, biases, Wp, bp):
     """bf16 MLP mode of DFM.py:104-137: table rows, weights and stored hidden
     activations rounded to bf16; accumulation and the final dot in fp32; FM
@@ -169,3 +184,24 @@ def dfm_bf16_out(X, E, w, layers, biases, Wp, bp):
             h = bf16_round(h)
     cat = np.concatenate([y1, y2, h], 1)
     return (cat @ Wp.reshape(-1, 1))[:, 0] + np.float32(bp)
+
+
+# ---------------------------------------------------------------------------
+# AFM rows (K4)
+# ---------------------------------------------------------------------------
+def afm_rows_exact(X, E, w, w0, W, b, pvec, P):
+    """float64 AFM.out of AFM.py:103-142 (attention on, keep = [1, 1]) and
+    its natural magnitude Σ_pairs att·Σ_c |(e_i ⊙ e_j)_c P_c| + Σ|w| + |w0|."""
+    X = np.asarray(X, np.int64)
+    e = np.asarray(E, np.float64)[X]
+    F = e.shape[1]
+    pr = np.stack([e[:, i] * e[:, j] for i in range(F) for j in range(i + 1, F)], 1)
+    z = pr @ np.asarray(W, np.float64) + np.asarray(b, np.float64).reshape(-1)
+    logit = (np.maximum(z, 0) * np.asarray(pvec, np.float64).reshape(-1)).sum(-1)
+    ex = np.exp(logit - logit.max(1, keepdims=True))
+    att = ex / ex.sum(1, keepdims=True)
+    t = att[:, :, None] * pr * np.asarray(P, np.float64).reshape(1, 1, -1)
+    fb = np.asarray(w, np.float64).reshape(-1)[X]
+    out = t.sum((1, 2)) + fb.sum(1) + float(w0)
+    mag = np.abs(t).sum((1, 2)) + np.abs(fb).sum(1) + abs(float(w0))
+    return out, mag

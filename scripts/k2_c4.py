@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """K2 at the C4 per-GPU shape (HHFM k=128, 1,024 queries x 1.25M-item shard,
 top-20): median kernel time per variant (HIP events), fp32 and bf16 tables.
-Variants are environment switches read per call (HHFM_CATALOG_SEED,
-HHFM_CATALOG_EXACT, HHFM_CATALOG_RING, HHFM_RING_PIPE=0 via "nopipe").  usage: python scripts/k2_c4.py [--reps N]"""
+Variants are plan flags (include/hhfm.h): "noseed" PLAN_NO_SEED, "exact"
+PLAN_EXACT_FP32, "noring" PLAN_NO_RING, "ringalt" PLAN_RING_ALT.
+usage: python scripts/k2_c4.py [--reps N] [--variants seed,noring,...]"""
 import argparse
 import json
 import os
@@ -37,14 +38,14 @@ def main():
     for tname, E in (("fp32", E32), ("bf16", E32.to(torch.bfloat16))):
         ref = None
         for var in a.variants.split(","):
-            os.environ["HHFM_CATALOG_SEED"] = "0" if "noseed" in var else "1"
-            os.environ["HHFM_CATALOG_EXACT"] = "1" if "exact" in var else "0"
-            os.environ["HHFM_CATALOG_RING"] = "0" if "noring" in var else "1"
-            os.environ["HHFM_RING_PIPE"] = "0" if "nopipe" in var else "1"
+            plan = ((ops.PLAN_NO_SEED if "noseed" in var else 0) |
+                    (ops.PLAN_EXACT_FP32 if "exact" in var else 0) |
+                    (ops.PLAN_NO_RING if "noring" in var else 0) |
+                    (ops.PLAN_RING_ALT if "ringalt" in var else 0))
 
             def run():
                 return ops.catalog_topk(A, E, ops.MODE_HHFM, K, nu + 12, N, 0, None, 0,
-                                        (2, 5), (0, 0))
+                                        (2, 5), (0, 0), plan=plan)
             run()
             torch.cuda.synchronize()
             ts = []

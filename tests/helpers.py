@@ -57,3 +57,32 @@ def topk_tie_swaps(got_i, ref_i, exact, window=TIE_WINDOW):
     n = _parity.topk_tie_swaps(got_i, ref_i, exact, window)
     log_parity("topk_tie_swaps", swaps=int(n), positions=int(np.asarray(got_i).size))
     return n
+
+
+def kappa_check(kind, got, ref32, exact, mag, rtol=1e-5, kappa_max=_parity.KAPPA_MAX):
+    """north_star 1e-5 *relative*, elementwise: every row whose condition
+    number κ = Σ|terms| / |exact| is at most ``kappa_max`` must be within
+    ``rtol`` of its float64 value ``exact``; beyond that fp32 itself cannot
+    promise 1e-5 relative, so those rows are held to ``rtol`` of Σ|terms|
+    (normwise) and their error is logged beside the fp32 oracle's (``ref32``)
+    own.  The per-case record goes to the parity report (conftest)."""
+    got = np.asarray(got, np.float64).reshape(-1)
+    ex = np.asarray(exact, np.float64).reshape(-1)
+    mag = np.asarray(mag, np.float64).reshape(-1)
+    den = np.maximum(np.abs(ex), 1e-300)
+    kappa = mag / den
+    rel_gpu = np.abs(got - ex) / den
+    ok = kappa <= kappa_max
+    rec = dict(rows=int(ok.size), rows_kappa_gt_100=int((~ok).sum()),
+               max_rel_err_kappa_le_100=float(rel_gpu[ok].max()) if ok.any() else 0.0,
+               max_rel_err_kappa_gt_100=float(rel_gpu[~ok].max()) if (~ok).any() else 0.0,
+               oracle_max_rel_err_kappa_gt_100=0.0)
+    if ref32 is not None and (~ok).any():
+        r32 = np.asarray(ref32, np.float64).reshape(-1)
+        rec["oracle_max_rel_err_kappa_gt_100"] = float((np.abs(r32 - ex) / den)[~ok].max())
+    log_parity(kind, **rec)
+    if ok.any():
+        assert rel_gpu[ok].max() <= rtol, (kind, float(rel_gpu[ok].max()))
+    norm = np.abs(got - ex) / np.maximum(mag, 1e-300)
+    assert norm.max() <= rtol, (kind, "normwise", float(norm.max()))
+    return rec

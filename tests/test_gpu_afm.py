@@ -1,7 +1,11 @@
 """AFM (K4) on the GPU vs the reference graph (golden afm.npz) and vs the
 oracle at Frappe shape.  fp32 numerics (exact-fp32 MFMA, or split-bf16 MFMA
-for the fused rows kernel when k % 16 == 0 — HHFM_AFM_EXACT=1 forces the
-former); tolerance 1e-5 of the natural magnitude of each reduction."""
+for the fused kernels when k % 16 == 0 — PLAN_EXACT_FP32 forces the former).
+Rows: 1e-5 relative of the float64 value of AFM.py:103-142, elementwise on
+every row whose condition number Σ|terms| / |out| is at most 100, normwise
+on the rest (tests/helpers.kappa_check; κ counts in the parity report).
+Catalog: top-K positions exact except fp32 ties within 1e-5 of the query's
+score scale."""
 import os
 
 import numpy as np
@@ -9,6 +13,8 @@ import pytest
 import torch
 
 from oracle import fm_oracle as orc
+from oracle import parity
+from tests.helpers import kappa_check
 
 pytestmark = pytest.mark.gpu
 G = os.path.join(os.path.dirname(__file__), "golden")
@@ -29,8 +35,9 @@ def test_afm_vs_reference_graph():
                   attention_W=d["attention_W"], attention_b=d["attention_b"],
                   attention_p=d["attention_p"], prediction=d["prediction"])
     out = m.score_rows(d["X"])[:, 0]
-    scale = np.abs(d["out"]).max()
-    assert np.allclose(out, d["out"], rtol=1e-5, atol=1e-5 * scale)
+    ex, mag = parity.afm_rows_exact(d["X"], d["E"], d["w"], d["w0"], d["attention_W"],
+                                    d["attention_b"], d["attention_p"], d["prediction"])
+    kappa_check("afm_rows_kappa", out, d["out"], ex, mag)
     out2 = m.sess.run(m.out, feed_dict={m.train_features: d["X"], m.train_labels: None,
                                          m.dropout_keep: [1.0, 1.0], m.train_phase: False})
     assert np.array_equal(out2[:, 0], out)
@@ -40,9 +47,10 @@ def test_afm_vs_reference_graph():
 
 
 @pytest.mark.parametrize("exact", ["0", "1"])
-@pytest.mark.parametrize("k,A", [(64, 64), (32, 16), (128, 128), (64, 32), (24, 32)])
-def test_afm_frappe_shape(k, A, exact, monkeypatch):
-    monkeypatch.setenv("HHFM_AFM_EXACT", exact)
+@pytest.mark.parametrize("k,A", [(64, 64), (32, 16), (128, 128), (64, 32), (24, 32), (48, 48)])
+def test_afm_frappe_shape(k, A, exact):
+    from hhfm_amd import ops
+    plan = ops.PLAN_EXACT_FP32 if exact == "1" else 0
     rng = np.random.default_rng(k + A)
     nu, ni = 957, 4082
     M = nu + ni + 12
@@ -54,15 +62,29 @@ def test_afm_frappe_shape(k, A, exact, monkeypatch):
                   rng.integers(nu + ni, nu + ni + 7, 700), rng.integers(nu + ni + 7, nu + ni + 9, 700),
                   rng.integers(nu + ni + 9, M, 700)], 1).astype(np.int32)
     args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
-    ref = orc.afm_out(X, W["feature_embeddings"], W["feature_bias"][:, 0], 0.0, *args)[:, 0]
-    got = m.score_rows(X)[:, 0]
-    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    E, w = W["feature_embeddings"], W["feature_bias"][:, 0]
+    ref = orc.afm_out(X, E, w, 0.0, *args)[:, 0]
+    Wt, b, p, P = m._att()
+    Xd = torch.from_numpy(X).cuda()
+    got = ops.afm_forward(Xd, m.table, m.weights["feature_bias"].reshape(-1), 0.0, Wt, b, p, P,
+                          plan=plan).cpu().numpy()
+    ex, mag = parity.afm_rows_exact(X, E, w, 0.0, *args)
+    kappa_check("afm_rows_kappa", got, ref, ex, mag)
     A_ = X[:40]
-    sc = orc.afm_catalog_scores(A_, W["feature_embeddings"], W["feature_bias"][:, 0], *args, nu, ni)
-    pred = m.topk(A_, 20)
+    sc = orc.afm_catalog_scores(A_, E, w, *args, nu, ni)
     rs, ri = orc.top_k(sc, 20)
-    bad, swaps = orc.topk_swaps(sc, ri, pred, 1e-5 * np.abs(sc).max(1, keepdims=True))
-    assert bad == 0 and swaps == 0, (bad, swaps)
+    # the default per-query kernel (folded weights) and the per-field one
+    for cplan in (plan, plan | ops.PLAN_PER_FIELD):
+        s_, pred = ops.afm_catalog_topk(torch.from_numpy(A_).cuda(), m.table,
+                                        m.weights["feature_bias"].reshape(-1), Wt, b, p, P, nu,
+                                        ni, 20, 0, plan=cplan)
+        pred = pred.cpu().numpy()
+        bad, swaps = orc.topk_swaps(sc, ri, pred, 1e-5 * np.abs(sc).max(1, keepdims=True))
+        assert bad == 0 and swaps == 0, (cplan, bad, swaps)
+        # returned scores: 1e-5 relative of the oracle's score of that item
+        picked = np.take_along_axis(sc, pred.astype(np.int64), 1)
+        rel = np.abs(s_.cpu().numpy() - picked) / np.maximum(np.abs(picked), 1e-30)
+        assert rel.max() <= 1e-5, (cplan, float(rel.max()))
 
 
 def test_afm_catalog_query_chunks():
@@ -110,7 +132,8 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
     ref = orc.afm_out(X, E, W["feature_bias"][:, 0], 0.0, *args)[:, 0]
     got = m.score_rows(X)[:, 0]
-    assert np.allclose(got, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+    ex, mag = parity.afm_rows_exact(X, E, W["feature_bias"][:, 0], 0.0, *args)
+    kappa_check("afm_rows_kappa", got, ref, ex, mag)
 
 
 @pytest.mark.parametrize("F,k,A,tdt,nq,ni,K", [
@@ -122,9 +145,14 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     (5, 20, 16, "f32", 13, 400, 20),      # GEMM path: k % 8 != 0
     (5, 128, 128, "f32", 6, 300, 20),     # fused: 75 KB of LDS (raised dynamic limit)
     (12, 64, 64, "f32", 7, 250, 20),      # GEMM path: 11 query fields (F = 12 datasets)
+    (5, 48, 48, "f32", 17, 901, 20),      # per-query kernel at k = 48 (U2 = 6 swizzle)
+    (3, 48, 40, "f32", 33, 777, 20),      # ... A padded to 64, two query fields
 ])
 def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
-    """A2 across the fused kernel's envelope and the GEMM path beyond it."""
+    """A2 across the fused kernels' envelope (the per-query kernel with the
+    folded weights by default, the per-field kernel with PLAN_PER_FIELD) and
+    the GEMM path (PLAN_GEMM, and every shape beyond the fused envelope)."""
+    from hhfm_amd import ops
     from tests.helpers import bf16_round
     rng = np.random.default_rng(F * 1000 + k + A)
     nu = 60
@@ -141,8 +169,18 @@ def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
         E = bf16_round(E)
     args = (W["attention_W"], W["attention_b"], W["attention_p"], W["prediction"])
     sc = orc.afm_catalog_scores(A_, E, W["feature_bias"][:, 0], *args, nu, ni)
-    pred = m.topk(A_, K)
     rs, ri = orc.top_k(sc, K)
-    bad, swaps = orc.topk_swaps(sc, ri, pred,
-                                         1e-5 * np.abs(sc).max(1, keepdims=True))
+    pred = m.topk(A_, K)
+    bad, swaps = orc.topk_swaps(sc, ri, pred, 1e-5 * np.abs(sc).max(1, keepdims=True))
     assert bad == 0 and swaps == 0, (bad, swaps)
+    Wt, b, p, P = m._att()
+    q = torch.from_numpy(A_).cuda()
+    for plan in (ops.PLAN_PER_FIELD, ops.PLAN_GEMM):
+        s_, i_ = ops.afm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, b, p,
+                                      P, nu, ni, K, 0, plan=plan)
+        i_ = i_.cpu().numpy()
+        bad, swaps = orc.topk_swaps(sc, ri, i_, 1e-5 * np.abs(sc).max(1, keepdims=True))
+        assert bad == 0 and swaps == 0, (plan, bad, swaps)
+        picked = np.take_along_axis(sc, i_.astype(np.int64), 1)
+        rel = np.abs(s_.cpu().numpy() - picked) / np.maximum(np.abs(picked), 1e-30)
+        assert rel.max() <= 1e-5, (plan, float(rel.max()))

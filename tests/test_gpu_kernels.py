@@ -217,16 +217,17 @@ def test_catalog_topk_hhfm_parity(dtype, k, K):
                        hhfm_exact(A, E, n_user)) <= MAX_TIES
 
 
-@pytest.mark.parametrize("variant", ["split", "exact", "gemm"])
+@pytest.mark.parametrize("variant", ["split", "exact", "gemm", "one_wave"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("k", [16, 64])
-def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
+def test_catalog_topk_fm_parity(dtype, k, variant):
     """Dense (score-matrix) path: the catalog kernel's STORE variant on
-    split-bf16 MFMA (default) or fp32 MFMA (HHFM_CATALOG_EXACT=1), or the
-    shared fp32 GEMM (HHFM_CATALOG_DENSE_GEMM=1), then the dense top-K."""
+    split-bf16 MFMA (default) or fp32 MFMA (PLAN_EXACT_FP32), or the shared
+    fp32 GEMM (PLAN_GEMM), then the dense top-K (4 waves per query, or one:
+    PLAN_ONE_WAVE)."""
     from hhfm_amd import ops
-    monkeypatch.setenv("HHFM_CATALOG_EXACT", "1" if variant == "exact" else "0")
-    monkeypatch.setenv("HHFM_CATALOG_DENSE_GEMM", "1" if variant == "gemm" else "0")
+    plan = {"split": 0, "exact": ops.PLAN_EXACT_FP32, "gemm": ops.PLAN_GEMM,
+            "one_wave": ops.PLAN_ONE_WAVE}[variant]
     rng = np.random.default_rng(5 + k)
     n_user, n_item = 957, 4082
     A, M = synth_rows(rng, 257, n_user, n_item, (7, 2, 3))
@@ -236,7 +237,7 @@ def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
     if dtype == "bf16":
         E = bf16_round(E)
     s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_FM, 20, n_user, n_item, 0,
-                            _dev(w), 0, (2, 5), (0, 0))
+                            _dev(w), 0, (2, 5), (0, 0), plan=plan)
     ref = orc.fm_catalog_scores(A, E, w, n_user, n_item)
     f = E[A[:, 2:].astype(np.int64)].sum(1)
     q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
@@ -250,13 +251,13 @@ def test_catalog_topk_fm_parity(dtype, k, variant, monkeypatch):
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("k,K", [(16, 5), (32, 1), (128, 20), (64, 64)])
-def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
+def test_catalog_topk_streaming_path(mode, dtype, k, K, exact):
     """Catalogs above the small-catalog bound (N > 16384) take the streaming
     threshold kernel (split-bf16 MFMA by default, the fp32-MFMA fmaf chain
-    with HHFM_CATALOG_EXACT=1); the
-    4082-item cases above take the dense score matrix."""
+    with PLAN_EXACT_FP32); the 4082-item cases above take the dense score
+    matrix."""
     from hhfm_amd import ops
-    monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
+    plan = ops.PLAN_EXACT_FP32 if exact == "1" else 0
     rng = np.random.default_rng(17 + k + K)
     n_user, n_item = 300, 20000
     A, M = synth_rows(rng, 70, n_user, n_item, (7, 2, 3))
@@ -266,14 +267,14 @@ def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
         E = bf16_round(E)
     if mode == "hhfm":
         s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, n_user, n_item, 0,
-                                None, 0, (2, 5), (0, 0))
+                                None, 0, (2, 5), (0, 0), plan=plan)
         ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
         scale = _hhfm_scale(A, E, n_user, n_item)
         exact = hhfm_exact(A, E, n_user)
     else:
         w = rng.normal(0, 0.01, size=M).astype(np.float32)
         s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_FM, K, n_user, n_item, 0,
-                                _dev(w), 0, (2, 5), (0, 0))
+                                _dev(w), 0, (2, 5), (0, 0), plan=plan)
         ref = orc.fm_catalog_scores(A, E, w, n_user, n_item)
         f = E[A[:, 2:].astype(np.int64)].sum(1)
         q = np.abs((E[A[:, 0].astype(np.int64)] + f).astype(np.float64))
@@ -284,13 +285,13 @@ def test_catalog_topk_streaming_path(mode, dtype, k, K, exact, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
-@pytest.mark.parametrize("small", ["1", "0"])
-def test_catalog_topk_small_path_ragged_shard(mode, small, monkeypatch):
-    """Small-catalog kernel (opt-in, HHFM_CATALOG_SMALL=1) and the default
-    GEMM + dense top-K path on a ragged shard: N % 16 != 0, non-zero row and global
-    bases, B % 16 != 0, item splits + merge."""
+@pytest.mark.parametrize("variant", ["store", "gemm"])
+def test_catalog_topk_small_path_ragged_shard(mode, variant):
+    """Small-catalog (dense score matrix) path, the catalog kernel's STORE
+    variant and the shared GEMM (PLAN_GEMM), on a ragged shard: N % 32 != 0,
+    non-zero row and global bases, B % 16 != 0."""
     from hhfm_amd import ops
-    monkeypatch.setenv("HHFM_CATALOG_SMALL", small)
+    plan = ops.PLAN_GEMM if variant == "gemm" else 0
     rng = np.random.default_rng(23)
     n_user, n_item, k = 400, 5000, 64
     A, M = synth_rows(rng, 37, n_user, n_item, (7, 2, 3))
@@ -299,7 +300,7 @@ def test_catalog_topk_small_path_ragged_shard(mode, small, monkeypatch):
     lo, cnt, gbase = n_user + 777, 1001, 777
     m = ops.MODE_HHFM if mode == "hhfm" else ops.MODE_FM
     s, i = ops.catalog_topk(_dev(A), _dev(E), m, 20, lo, cnt, gbase,
-                            _dev(w) if mode == "fm" else None, 0, (2, 5), (0, 0))
+                            _dev(w) if mode == "fm" else None, 0, (2, 5), (0, 0), plan=plan)
     if mode == "hhfm":
         full = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
         scale = _hhfm_scale(A, E, n_user, n_item)
@@ -361,7 +362,7 @@ def test_topk_merge_device_matches_host():
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_catalog_topk_c4_shard(dtype, monkeypatch):
+def test_catalog_topk_c4_shard(dtype):
     """configs[3] (C4) per-GPU shape: HHFM k=128, a 1.25M-item shard of a
     10M-item catalog (rank 3 of 8: global_item_base 3.75M, item rows not at
     n_user), 1,024 queries, top-20; split-bf16 and exact-fp32 kernels against
@@ -386,9 +387,9 @@ def test_catalog_topk_c4_shard(dtype, monkeypatch):
     ri = ri + gbase
     exact = hhfm_exact(A, E, nu + pre - gbase)
     for variant in ("0", "1"):
-        monkeypatch.setenv("HHFM_CATALOG_EXACT", variant)
         s, i = ops.catalog_topk(_dev(A), Eg, ops.MODE_HHFM, K, nu + pre, shard, gbase,
-                                None, 0, (2, 5), (0, 0))
+                                None, 0, (2, 5), (0, 0),
+                                plan=ops.PLAN_EXACT_FP32 if variant == "1" else 0)
         s, i = s.cpu().numpy(), i.cpu().numpy()
         swaps = topk_tie_swaps(i, ri, exact)
         assert i.min() >= gbase and i.max() < gbase + shard
@@ -406,14 +407,16 @@ def test_catalog_topk_c4_shard(dtype, monkeypatch):
 @pytest.mark.parametrize("exact", ["0", "1"])
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
 @pytest.mark.parametrize("dtype,k", [("f32", 128), ("bf16", 64), ("bf16", 128)])
-def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact, monkeypatch):
+def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact):
     """The streaming path's threshold seed (exact top-K of the first 32,768
     items from the STORE score matrix) only drops items that cannot reach the
-    top-K: seeded and unseeded runs return the same bits, and both match the
-    C oracle (shard with non-zero row and global bases, K = 20 and 64)."""
+    top-K: seeded and unseeded (PLAN_NO_SEED) runs return the same bits, and
+    both match the C oracle (shard with non-zero row and global bases, K = 20
+    and 64); where the ring kernel runs, catalog_main (PLAN_NO_RING) and the
+    other ring workgroup size (PLAN_RING_ALT) return the same bits too."""
     from hhfm_amd import ops
     from oracle import cpu as ocpu
-    monkeypatch.setenv("HHFM_CATALOG_EXACT", exact)
+    xp = ops.PLAN_EXACT_FP32 if exact == "1" else 0
     rng = np.random.default_rng(41)
     nu, pre, N, B = 700, 333, 600_000, 300
     M = nu + pre + N + 12
@@ -431,22 +434,21 @@ def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact, monkeypatch
     for K in (20, 64):
         res = {}
         for seed in ("1", "0"):
-            monkeypatch.setenv("HHFM_CATALOG_SEED", seed)
-            s, i = ops.catalog_topk(_dev(A), Eg, m, K, nu + pre, N, 5000, wd, 0, (2, 5), (0, 0))
+            plan = xp | (0 if seed == "1" else ops.PLAN_NO_SEED)
+            s, i = ops.catalog_topk(_dev(A), Eg, m, K, nu + pre, N, 5000, wd, 0, (2, 5), (0, 0),
+                                    plan=plan)
             res[seed] = (s.cpu().numpy(), i.cpu().numpy())
         assert np.array_equal(res["1"][0].view(np.int32), res["0"][0].view(np.int32))
         assert np.array_equal(res["1"][1], res["0"][1])
         if K <= 32 and exact == "0" and k >= (128 if dtype == "bf16" else 64):
-            # catalog_ring (seeded, split-bf16, K <= 32) at 4 and 8 waves per
-            # workgroup: B = 300 leaves idle waves in the last query block
-            monkeypatch.setenv("HHFM_CATALOG_SEED", "1")
-            for waves in ("4", "8"):
-                monkeypatch.setenv("HHFM_RING_WAVES", waves)
+            # catalog_ring (seeded, split-bf16, K <= 32) at its other workgroup
+            # size (B = 300 leaves idle waves in the last query block) and
+            # catalog_main instead of the ring
+            for plan in (ops.PLAN_RING_ALT, ops.PLAN_NO_RING):
                 s, i = ops.catalog_topk(_dev(A), Eg, m, K, nu + pre, N, 5000, wd, 0, (2, 5),
-                                        (0, 0))
+                                        (0, 0), plan=plan)
                 assert np.array_equal(s.cpu().numpy().view(np.int32), res["1"][0].view(np.int32))
                 assert np.array_equal(i.cpu().numpy(), res["1"][1])
-            monkeypatch.delenv("HHFM_RING_WAVES")
         rs, ri = ocpu.catalog_topk(A, E, 0 if mode == "fm" else 1, K, nu + pre, N,
                                    w=w if mode == "fm" else None, ctx=(2, 5), threads=16)
         exact_fn = (fm_exact(A, E, w, nu + pre - 5000) if mode == "fm"
