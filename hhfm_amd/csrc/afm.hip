@@ -966,7 +966,9 @@ static AfmCatPlan afm_cat_plan(int64_t B, int F, int k, int A, int N, int64_t ma
     p.total = off;
     return p;
   }
-  p.G = A < 64 ? A : 64;
+  // logit groups of the grouped-dot epilogue: 16, 32 or 64 columns that
+  // divide A (a group never straddles two (query, field) column blocks)
+  p.G = A % 64 == 0 ? 64 : (A % 32 == 0 ? 32 : 16);
   int64_t qc = max_cols / ((int64_t)uF * A);
   if (qc < 1) qc = 1;
   if (qc > B) qc = B;
@@ -1140,7 +1142,7 @@ extern "C" int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t 
     return HHFM_EINVAL;
   if (K < 1 || K > item_count) return HHFM_EINVAL;
   if (K > 64) return HHFM_EUNSUPPORTED;
-  if (!afm_cat_fused_ok(F, k, A, plan) && (k % 4 || A % 16 || (A > 64 && A % 64)))
+  if (!afm_cat_fused_ok(F, k, A, plan) && (k % 4 || A % 16))
     return HHFM_EUNSUPPORTED;
   if (B == 0) return HHFM_OK;
   if (!qidx || !E || !w || !Wt || !att_b || !att_p || !P || !top_score || !top_idx)

@@ -318,7 +318,7 @@ int hhfm_afm_forward_ex(const int32_t* idx, int64_t B, int32_t F, const void* E,
  * pair attention over uf pairs and uf x item pairs (raw exp, as the
  * reference), score = (Σ_c P_c·score1_c) / weight + w_item, then top-K.
  * At most max_cols = (queries per pass)·(F-1)·A GEMM columns per pass.
- * k <= 256, k % 4 == 0, A % 16 == 0 (and A % 64 == 0 when A > 64), F <= 16. */
+ * k <= 256, k % 4 == 0, A % 16 == 0 (or inside the fused envelope), F <= 16. */
 int hhfm_afm_catalog_topk_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
                                     int32_t item_count, int64_t max_cols,
                                     size_t* ws_bytes);

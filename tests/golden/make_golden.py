@@ -19,6 +19,9 @@ Frappe README forbids redistribution):
   losses.npz            each model's `self.loss` at seeded weights + batch
   harness.npz + harness.json               sample_negative / evaluate_TopK /
                                            evaluate_AUC outputs
+  epoch_stream.json     the batches the reference's own Train.train feeds
+                        partial_fit (FM and OurModel7, 2 epochs on
+                        synth_frappe, seeded): per-batch sha256 of X/Y/F1
 Usage:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
 """
 from __future__ import annotations
@@ -392,6 +395,52 @@ def gen_harness(d):
     print("harness", res)
 
 
+class _Recorder:
+    """Stand-in model whose partial_fit records each batch it is fed (the
+    epoch loop, not the model, is under test) and returns a fixed loss."""
+
+    def __init__(self):
+        self.batches = []
+
+    def partial_fit(self, data):
+        import hashlib
+        h = hashlib.sha256()
+        for key in sorted(data):
+            a = np.ascontiguousarray(np.asarray(data[key], dtype=np.float64))
+            h.update(key.encode())
+            h.update(np.asarray(a.shape, np.int64).tobytes())
+            h.update(a.tobytes())
+        self.batches.append(h.hexdigest())
+        return 1.0
+
+
+def epoch_stream_case(mod, seed, epochs=2, batch=512):
+    """The reference's Train.train (FM.py:221-282 / OurModel7.py:349-413),
+    unmodified, with Result = 1 (no evaluation before epoch 30 / 20) and a
+    recording model, on a fresh seeded LoadData of synth_frappe."""
+    import argparse
+    np.random.seed(2016)
+    d = NLD.LoadData(os.path.join(HERE) + "/", "synth_frappe")
+    t = object.__new__(mod.Train)
+    t.args = argparse.Namespace(Result=1, dataset="synth_frappe", verbose=0)
+    t.data, t.n_user, t.n_item = d, d.n_user, d.n_item
+    t.epoch, t.batch_size, t.verbose, t.TopK = epochs + 1, batch, 0, 10
+    t.context, t.time, t.time_dimension = True, False, 0
+    t.model = _Recorder()
+    np.random.seed(seed)
+    t.train()
+    return t.model.batches
+
+
+def gen_epoch_stream():
+    res = {"fm": epoch_stream_case(RFM, 41), "hhfm": epoch_stream_case(RM7, 43),
+           "epochs": 2, "batch_size": 512, "seeds": {"fm": 41, "hhfm": 43},
+           "loaddata_seed": 2016}
+    with open(os.path.join(HERE, "epoch_stream.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    print("epoch_stream", {k: len(v) for k, v in res.items() if isinstance(v, list)})
+
+
 def gen_frappe_real():
     """Real Frappe (builder container only): commit only derived numbers —
     split hashes and the reference harness's HR/NDCG/PRE@10 for a seeded
@@ -432,6 +481,7 @@ def main():
     gen_dfm()
     gen_losses()
     gen_harness(d)
+    gen_epoch_stream()
     gen_frappe_real()
 
 

@@ -147,6 +147,7 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     (12, 64, 64, "f32", 7, 250, 20),      # GEMM path: 11 query fields (F = 12 datasets)
     (5, 48, 48, "f32", 17, 901, 20),      # per-query kernel at k = 48 (U2 = 6 swizzle)
     (3, 48, 40, "f32", 33, 777, 20),      # ... A padded to 64, two query fields
+    (5, 32, 96, "f32", 9, 555, 20),       # A = 96: 32-column logit groups on the GEMM path
 ])
 def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
     """A2 across the fused kernels' envelope (the per-query kernel with the
@@ -175,7 +176,8 @@ def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
     assert bad == 0 and swaps == 0, (bad, swaps)
     Wt, b, p, P = m._att()
     q = torch.from_numpy(A_).cuda()
-    for plan in (ops.PLAN_PER_FIELD, ops.PLAN_GEMM):
+    gemm_ok = A % 16 == 0   # the GEMM path's envelope
+    for plan in (ops.PLAN_PER_FIELD,) + ((ops.PLAN_GEMM,) if gemm_ok else ()):
         s_, i_ = ops.afm_catalog_topk(q, m.table, m.weights["feature_bias"].reshape(-1), Wt, b, p,
                                       P, nu, ni, K, 0, plan=plan)
         i_ = i_.cpu().numpy()

@@ -218,3 +218,31 @@ def test_afm_train_loop_end_to_end(tmp_path):
     losses = t.train()
     assert len(losses) == 2 and losses[1] < losses[0]
     assert "AFM Epoch 1" in open(tmp_path / "result.txt").read()
+
+
+@pytest.mark.parametrize("entry", ["FM_main", "M7_main", "AFM_main", "DFM_main"])
+def test_main_entry_points_through_argv(entry, tmp_path):
+    """main.py's surface (Newcode/main.py:47-63 calls X_main(dataname, factor,
+    TopK)): each entry point parses the reference's flags from argv, loads
+    synth_frappe through LoadData, trains one epoch on the GPU (the loop
+    whose batch stream test_epoch_stream.py pins) and appends the
+    reference's result lines (Init + epoch 1 at --verbose 1; HHFM evaluates
+    at init only before epoch 10, OurModel7.py:404) to --result_file."""
+    import importlib
+    mod = {"FM_main": "FM", "M7_main": "OurModel7", "AFM_main": "AFM", "DFM_main": "DFM"}[entry]
+    fn = getattr(importlib.import_module(f"hhfm_amd.{mod}"), entry)
+    out = tmp_path / "result.txt"
+    argv = ["--path", G + "/", "--epoch", "2", "--batch_size", "4096",
+            "--result_file", str(out)]
+    if entry != "M7_main":
+        argv += ["--verbose", "1"]
+    np.random.seed(2016)
+    session = fn("synth_frappe", 16, 5, argv)
+    assert len(session.loss_epoch) == 1 and np.isfinite(session.loss_epoch[0])
+    lines = out.read_text().splitlines()
+    assert lines[0].startswith("Dataset=synth_frappe ") and "Init:" in lines[0]
+    assert len(lines) == (1 if entry == "M7_main" else 2), lines
+    for ln in lines:
+        auc = float(ln.split("train=AUC:")[1].split(";")[0])
+        hr = float(ln.split("HR:")[1].split(",")[0])
+        assert 0.0 <= auc <= 1.0 and 0.0 <= hr <= 1.0, ln
