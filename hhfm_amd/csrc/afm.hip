@@ -355,6 +355,199 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
   }
 }
 
+// ---- A1 pair-major: one wave = 32 rows, one MFMA tile column per row ---------
+// The transposed pre-activations D[unit][row] = Σ_k Wᵀ[unit][k]·(e_i⊙e_j)[row][k]
+// are computed for ONE pair (i, j) of 32 rows at a time (split-bf16 MFMA as
+// afm_rows_fused: Wᵀ as three bf16 LDS images, the pair product split in
+// registers per 16 k, the six piece products of order >= 2^-16), so lane j
+// (both halves) ends up holding row j's logit of that pair: relu(· + b)·p
+// summed over its 16 units per tile and the two lane halves, the bias the
+// accumulators' initial value.  The row's pair logits and pair scores
+// s = (e_i⊙e_j)·P are parked in a lane-private LDS slot per pair, and the
+// pair softmax (tf.nn.softmax, AFM.py:125) + Σ_p att_p·s_p runs in-lane for
+// the 32 rows at once — no per-row serial epilogue, all 32 columns live
+// (afm_rows_fused packs floor(32/np) rows of np pairs: 30 of 32 at F = 5,
+// and its softmax runs one lane per row).  F <= 8 (np <= 28 slots).
+constexpr int kAfmPairSlots = 28;
+
+static size_t afm_rows_pairs_lds(int NA, int K) {
+  return (size_t)3 * NA * K * 2 + 4 * (K + 2 * NA) + (size_t)4 * kAfmPairSlots * 32 * 8 +
+         (size_t)4 * kAfmFusedMaxF * 32 * 4;
+}
+
+template <bool TBF, int NT, int KS>
+__global__ __launch_bounds__(256, 2) void afm_rows_pairs(
+    const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
+    const float* __restrict__ w, float w0, const float* __restrict__ Wt,
+    const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
+    const float* __restrict__ P, float* __restrict__ out) {
+  constexpr int NA = NT * 32, K = 16 * KS, U2 = K / 8;
+  constexpr int SW2 = ((U2 & -U2) < 16 ? (U2 & -U2) : 16) - 1;   // largest pow2 | U2, <= 16
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // afm_rows_pairs_lds()
+  uint4* imgb = reinterpret_cast<uint4*>(smem);                   // [piece][unit][chunk]
+  float* Pl = smem + 3 * NA * U2 * 4;
+  float* bl = Pl + K;
+  float* apl = bl + NA;
+  float2* slots = reinterpret_cast<float2*>(apl + NA);            // [wave][pair][32]
+  int32_t* idl = reinterpret_cast<int32_t*>(slots + 4 * kAfmPairSlots * 32);   // [wave][f][32]
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int j = l & 31, h = l >> 5;
+  for (int x = tid; x < NA * U2; x += 256) {
+    const int u = x / U2, c = x - u * U2;
+    const int kb = 16 * (c >> 1) + 4 * (c & 1);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[e] = u < A ? Wt[(int64_t)u * K + kb + e] : 0.f;
+      v[4 + e] = u < A ? Wt[(int64_t)u * K + kb + 8 + e] : 0.f;
+    }
+    bf16x8 q0, q1, q2;
+    split3x8(v, q0, q1, q2);
+    const int o = u * U2 + (c ^ (u & SW2));
+    imgb[o] = __builtin_bit_cast(uint4, q0);
+    imgb[NA * U2 + o] = __builtin_bit_cast(uint4, q1);
+    imgb[2 * NA * U2 + o] = __builtin_bit_cast(uint4, q2);
+  }
+  for (int x = tid; x < K; x += 256) Pl[x] = P[x];
+  for (int x = tid; x < NA; x += 256) {
+    bl[x] = x < A ? att_b[x] : 0.f;
+    apl[x] = x < A ? att_p[x] : 0.f;
+  }
+  __syncthreads();
+
+  const int np = F * (F - 1) / 2;
+  float2* sl = slots + wv * kAfmPairSlots * 32;
+  int32_t* il = idl + wv * kAfmFusedMaxF * 32;
+  const int64_t nblk = (B + 31) / 32;
+  for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += (int64_t)gridDim.x * 4) {
+    const int64_t row = blk * 32 + j;
+    const bool ok = row < B;
+    const int64_t rr = ok ? row : B - 1;
+    float fb = 0.f;
+    if (h == 0)
+      for (int f = 0; f < F; ++f) {
+        const int32_t id = clamp_id(idx[rr * F + f], M);
+        il[f * 32 + j] = id;
+        fb += w[id];                                  // Σ_f w[x_f]   AFM.py:140
+      }
+    // (one wave's LDS accesses complete in order: the ids are read back below)
+    // this lane's 8 k of 16-k step t of table row `id`: {16t + 4h .. +3, 16t + 8 + 4h .. +3}
+    auto gather = [&](int32_t id, int t, float (&x)[8]) {
+      const int c0 = 16 * t + 4 * h;
+      if constexpr (TBF) {
+        const uint16_t* r = reinterpret_cast<const uint16_t*>(E) + (int64_t)id * K + c0;
+        const uint2 lo = *reinterpret_cast<const uint2*>(r), hi = *reinterpret_cast<const uint2*>(r + 8);
+        const uint32_t u4[4] = {lo.x, lo.y, hi.x, hi.y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x[2 * e] = __uint_as_float(u4[e] << 16);
+          x[2 * e + 1] = __uint_as_float(u4[e] & 0xffff0000u);
+        }
+      } else {
+        const float* r = reinterpret_cast<const float*>(E) + (int64_t)id * K + c0;
+        const float4 lo = *reinterpret_cast<const float4*>(r), hi = *reinterpret_cast<const float4*>(r + 8);
+        x[0] = lo.x; x[1] = lo.y; x[2] = lo.z; x[3] = lo.w;
+        x[4] = hi.x; x[5] = hi.y; x[6] = hi.z; x[7] = hi.w;
+      }
+    };
+    int pi = 0, pj = 1;
+    int32_t ia = il[j], ib = il[32 + j];
+    float xa[KS][8], ya[KS][8];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      gather(ia, t, xa[t]);
+      gather(ib, t, ya[t]);
+    }
+    for (int p = 0; p < np; ++p) {
+      // the next pair's rows (read now, gathered during this pair's MFMAs)
+      int ni = pi, nj = pj + 1;
+      if (nj == F) {
+        ++ni;
+        nj = ni + 1;
+      }
+      const bool more = p + 1 < np;
+      int32_t na = 0, nb = 0;
+      if (more) {
+        na = il[ni * 32 + j];
+        nb = il[nj * 32 + j];
+      }
+      // the accumulators' initial value: unit 32n + 8g4 + 4h + e's bias
+      f32x16 acc[NT];
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 b4 = *reinterpret_cast<const float4*>(bl + 32 * n + 8 * g4 + 4 * h);
+          acc[n][4 * g4 + 0] = b4.x;
+          acc[n][4 * g4 + 1] = b4.y;
+          acc[n][4 * g4 + 2] = b4.z;
+          acc[n][4 * g4 + 3] = b4.w;
+        }
+      float sP = 0.f;
+#pragma unroll
+      for (int t = 0; t < KS; ++t) {
+        float pe[8];
+        const int c0 = 16 * t + 4 * h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pe[e] = xa[t][e] * ya[t][e];
+          sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
+        }
+        if (more) {                                   // step t of the next pair
+          gather(na, t, xa[t]);
+          gather(nb, t, ya[t]);
+        }
+        bf16x8 b0, b1, b2;
+        split3x8(pe, b0, b1, b2);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int u = 32 * n + j;                   // A-operand row = attention unit
+          const int o = u * U2 + ((2 * t + h) ^ (u & SW2));
+          const bf16x8 a0 = __builtin_bit_cast(bf16x8, imgb[o]);
+          const bf16x8 a1 = __builtin_bit_cast(bf16x8, imgb[NA * U2 + o]);
+          const bf16x8 a2 = __builtin_bit_cast(bf16x8, imgb[2 * NA * U2 + o]);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[n], 0, 0, 0);
+        }
+      }
+      // the row's logit of this pair: Σ_units p·relu(acc)  (AFM.py:112-117)
+      float lg = 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 pq = *reinterpret_cast<const float4*>(apl + 32 * n + 8 * g4 + 4 * h);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 0], 0.f), pq.x, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 1], 0.f), pq.y, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 2], 0.f), pq.z, lg);
+          lg = fmaf(fmaxf(acc[n][4 * g4 + 3], 0.f), pq.w, lg);
+        }
+      lg += __shfl_xor(lg, 32, kWave);
+      sP += __shfl_xor(sP, 32, kWave);
+      if (h == 0) sl[p * 32 + j] = make_float2(lg, sP);
+      pi = ni;
+      pj = nj;
+    }
+    // softmax over the row's pairs + Σ_p att_p·s_p, in-lane (lane j = row j)
+    if (h == 0 && ok) {
+      float mx = kNegInf;
+      for (int p = 0; p < np; ++p) mx = fmaxf(mx, sl[p * 32 + j].x);
+      float se = 0.f, num = 0.f;
+      for (int p = 0; p < np; ++p) {
+        const float2 q = sl[p * 32 + j];
+        const float e = expf(q.x - mx);
+        se += e;
+        num = fmaf(e, q.y, num);
+      }
+      out[row] = (num / se + fb) + w0;                // add_n, AFM.py:142
+    }
+  }
+}
+
 // ---- A2 prep: one 64-thread block per query ------------------------------------
 // uf = [E[q0], E[q2], ..., E[q_{F-1}]] (u_f = F-1 fields, AFM.py:210-212)
 constexpr int kAfmMaxUF = 15;
@@ -1033,6 +1226,41 @@ extern "C" int hhfm_afm_forward_ex(const int32_t* idx, int64_t B, int32_t F, con
       const bool tb = dtype == HHFM_BF16;
       const bool split = k % 16 == 0 && !(plan & HHFM_PLAN_EXACT_FP32) &&
                          afm_rows_fused_lds(k, A, true) <= 160 * 1024;
+      // pair-major kernel (32 rows per wave tile): split arithmetic, k = 16·KS
+      // for KS in {2, 3, 4} (a whole pair's gathers in flight), A <= 96,
+      // F <= 8 (default; HHFM_PLAN_PER_FIELD keeps the combo-packed
+      // afm_rows_fused)
+      const int KSp = k / 16;
+      const size_t lp = afm_rows_pairs_lds(NT * 32, k);
+      if (split && !(plan & HHFM_PLAN_PER_FIELD) && KSp >= 2 && KSp <= 4 && NT <= 3 &&
+          lp <= 160 * 1024) {
+        const int64_t nb32 = (B + 31) / 32;
+        int64_t pblocks = (nb32 + 3) / 4;
+        if (pblocks > 2048) pblocks = 2048;
+#define HHFM_AFM_PAIRS_L(N, TB, KS)                                                          \
+  {                                                                                        \
+    allow_lds((const void*)afm_rows_pairs<TB, N, KS>, lp);                                  \
+    hipLaunchKernelGGL((afm_rows_pairs<TB, N, KS>), dim3((unsigned)pblocks), dim3(256), lp, \
+                       st, idx, B, F, E, features_M, w, w0, Wt, att_b, att_p, A, P, out);  \
+  }
+#define HHFM_AFM_PAIRS_K(N, TB)                      \
+  switch (KSp) {                                     \
+    case 2: HHFM_AFM_PAIRS_L(N, TB, 2) break;        \
+    case 3: HHFM_AFM_PAIRS_L(N, TB, 3) break;        \
+    default: HHFM_AFM_PAIRS_L(N, TB, 4) break;       \
+  }
+#define HHFM_AFM_PAIRS(N)                                                   \
+  if (NT == N) {                                                           \
+    if (tb) { HHFM_AFM_PAIRS_K(N, true) } else { HHFM_AFM_PAIRS_K(N, false) } \
+    return (int)hipGetLastError();                                         \
+  }
+        HHFM_AFM_PAIRS(1)
+        HHFM_AFM_PAIRS(2)
+        HHFM_AFM_PAIRS(3)
+#undef HHFM_AFM_PAIRS
+#undef HHFM_AFM_PAIRS_K
+#undef HHFM_AFM_PAIRS_L
+      }
       const size_t lds = afm_rows_fused_lds(k, A, split);
 #define HHFM_AFM_FUSED_K(N, TB, SP, KS)                                                      \
   {                                                                                        \
