@@ -367,16 +367,25 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
 // pair softmax (tf.nn.softmax, AFM.py:125) + Σ_p att_p·s_p runs in-lane for
 // the 32 rows at once — no per-row serial epilogue, all 32 columns live
 // (afm_rows_fused packs floor(32/np) rows of np pairs: 30 of 32 at F = 5,
-// and its softmax runs one lane per row).  F <= 8 (np <= 28 slots).
-constexpr int kAfmPairSlots = 28;
+// and its softmax runs one lane per row).  F <= 8.
+#ifndef HHFM_AFM_PAIR_PF
+#define HHFM_AFM_PAIR_PF 0   // gathers in flight: 0 = a whole pair ahead, 1 = one 16-k step
+#endif
+#ifndef HHFM_AFM_PAIR_OCC
+#define HHFM_AFM_PAIR_OCC 2  // __launch_bounds__ minimum workgroups per CU (A/B)
+#endif
 
-static size_t afm_rows_pairs_lds(int NA, int K) {
-  return (size_t)3 * NA * K * 2 + 4 * (K + 2 * NA) + (size_t)4 * kAfmPairSlots * 32 * 8 +
-         (size_t)4 * kAfmFusedMaxF * 32 * 4;
+// LDS: the three Wᵀ piece images, P, b, p, then per wave the rows' ids
+// [F][32] and the pair slots [np][32] (sized per call: F = 5 needs 40 KB at
+// k = A = 64, so four workgroups fit a CU)
+static size_t afm_rows_pairs_lds(int NA, int K, int F) {
+  const int np = F * (F - 1) / 2;
+  return (size_t)3 * NA * K * 2 + 4 * (K + 2 * NA) + (size_t)4 * F * 32 * 4 +
+         (size_t)4 * np * 32 * 8;
 }
 
 template <bool TBF, int NT, int KS>
-__global__ __launch_bounds__(256, 2) void afm_rows_pairs(
+__global__ __launch_bounds__(256, HHFM_AFM_PAIR_OCC) void afm_rows_pairs(
     const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
     const float* __restrict__ w, float w0, const float* __restrict__ Wt,
     const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
@@ -388,8 +397,8 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
   float* Pl = smem + 3 * NA * U2 * 4;
   float* bl = Pl + K;
   float* apl = bl + NA;
-  float2* slots = reinterpret_cast<float2*>(apl + NA);            // [wave][pair][32]
-  int32_t* idl = reinterpret_cast<int32_t*>(slots + 4 * kAfmPairSlots * 32);   // [wave][f][32]
+  int32_t* idl = reinterpret_cast<int32_t*>(apl + NA);            // [wave][f][32]
+  float2* slots = reinterpret_cast<float2*>(idl + 4 * F * 32);     // [wave][pair][32]
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int j = l & 31, h = l >> 5;
   for (int x = tid; x < NA * U2; x += 256) {
@@ -416,8 +425,8 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
   __syncthreads();
 
   const int np = F * (F - 1) / 2;
-  float2* sl = slots + wv * kAfmPairSlots * 32;
-  int32_t* il = idl + wv * kAfmFusedMaxF * 32;
+  float2* sl = slots + wv * np * 32;
+  int32_t* il = idl + wv * F * 32;
   const int64_t nblk = (B + 31) / 32;
   for (int64_t blk = (int64_t)blockIdx.x * 4 + wv; blk < nblk; blk += (int64_t)gridDim.x * 4) {
     const int64_t row = blk * 32 + j;
@@ -452,12 +461,21 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
     };
     int pi = 0, pj = 1;
     int32_t ia = il[j], ib = il[32 + j];
+#if HHFM_AFM_PAIR_PF == 1
+    // one 16-k step of gathers in flight (fewer registers)
+    float xa[1][8], ya[1][8];
+    gather(ia, 0, xa[0]);
+    gather(ib, 0, ya[0]);
+#else
+    // a whole pair's gathers in flight: step t of pair p+1 issued after step
+    // t of pair p consumed its registers
     float xa[KS][8], ya[KS][8];
 #pragma unroll
     for (int t = 0; t < KS; ++t) {
       gather(ia, t, xa[t]);
       gather(ib, t, ya[t]);
     }
+#endif
     for (int p = 0; p < np; ++p) {
       // the next pair's rows (read now, gathered during this pair's MFMAs)
       int ni = pi, nj = pj + 1;
@@ -488,6 +506,20 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
       for (int t = 0; t < KS; ++t) {
         float pe[8];
         const int c0 = 16 * t + 4 * h;
+#if HHFM_AFM_PAIR_PF == 1
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pe[e] = xa[0][e] * ya[0][e];
+          sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
+        }
+        if (t + 1 < KS) {                             // the next step
+          gather(ia, t + 1, xa[0]);
+          gather(ib, t + 1, ya[0]);
+        } else if (more) {                            // the next pair's first step
+          gather(na, 0, xa[0]);
+          gather(nb, 0, ya[0]);
+        }
+#else
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           pe[e] = xa[t][e] * ya[t][e];
@@ -497,6 +529,7 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
           gather(na, t, xa[t]);
           gather(nb, t, ya[t]);
         }
+#endif
         bf16x8 b0, b1, b2;
         split3x8(pe, b0, b1, b2);
 #pragma unroll
@@ -531,6 +564,8 @@ __global__ __launch_bounds__(256, 2) void afm_rows_pairs(
       if (h == 0) sl[p * 32 + j] = make_float2(lg, sP);
       pi = ni;
       pj = nj;
+      ia = na;
+      ib = nb;
     }
     // softmax over the row's pairs + Σ_p att_p·s_p, in-lane (lane j = row j)
     if (h == 0 && ok) {
@@ -1231,7 +1266,7 @@ extern "C" int hhfm_afm_forward_ex(const int32_t* idx, int64_t B, int32_t F, con
       // F <= 8 (default; HHFM_PLAN_PER_FIELD keeps the combo-packed
       // afm_rows_fused)
       const int KSp = k / 16;
-      const size_t lp = afm_rows_pairs_lds(NT * 32, k);
+      const size_t lp = afm_rows_pairs_lds(NT * 32, k, F);
       if (split && !(plan & HHFM_PLAN_PER_FIELD) && KSp >= 2 && KSp <= 4 && NT <= 3 &&
           lp <= 160 * 1024) {
         const int64_t nb32 = (B + 31) / 32;

@@ -1363,7 +1363,6 @@ __global__ __launch_bounds__(256) void dfm_fm_base_st(const int32_t* __restrict_
 // re-associated): one exact-fp32 MFMA GEMM per call (2·M²·k flops) instead of
 // reading every row's F table rows.  Rows grouped by user: a block's entries
 // of its user's row of C stay in L1/L2; the item's are one line per row.
-constexpr int kFmpStageB = 48 * 1024;
 __global__ __launch_bounds__(256) void dfm_scale_rows(const void* __restrict__ E, int tbf,
                                                       int64_t M, int k,
                                                       const float* __restrict__ wk,

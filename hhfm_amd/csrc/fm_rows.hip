@@ -40,21 +40,11 @@ HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
 // ---------------------------------------------------------------------------
 // FM row kernel: out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0
 // ---------------------------------------------------------------------------
-// HOT: the table's tail rows [hot_lo, M) — LoadData's context vocabulary
-// (NewLoadData.py:29-34 numbers users, then items, then the context values),
-// which every row gathers — are staged once per workgroup in LDS with their
-// w, and a hot id's 16-B chunk is read from there: the row loads become flat
-// loads whose address is the LDS copy or the table row (a select, no branch,
-// so the loads of one iteration still issue back to back; any hot_lo gives
-// the same bits).
-constexpr int kHotBytes = 16384;   // staged tail rows per workgroup (64 fp32 k=64 rows)
-constexpr int kHotRows = 256;      // and their w
-
-template <int F, int LPR, bool BF16, bool HAS_W, bool NT, bool HOT = false>
+template <int F, int LPR, bool BF16, bool HAS_W, bool NT>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
     int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out,
-    int32_t* __restrict__ status, int32_t hot_lo) {
+    int32_t* __restrict__ status) {
   constexpr int U = RowsPerLane<F>::value;
   constexpr int RPW = kWave / LPR;  // rows per wave per unroll slot
   constexpr int RPI = RPW * U;      // rows per wave-iteration
@@ -67,17 +57,6 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
   const int64_t nwave = ((int64_t)gridDim.x * blockDim.x) / kWave;
   const int64_t stride = nwave * RPI;
-
-  __shared__ u32x4_t hot_rows[HOT ? kHotBytes / 16 : 1];
-  __shared__ float hot_w[HOT ? kHotRows : 1];
-  if constexpr (HOT) {
-    const int nhot = (int)(M - hot_lo);
-    const u32x4_t* src = reinterpret_cast<const u32x4_t*>(E + (int64_t)hot_lo * ROW_BYTES);
-    for (int i = threadIdx.x; i < nhot * LPR; i += 256) hot_rows[i] = src[i];
-    if constexpr (HAS_W)
-      for (int i = threadIdx.x; i < nhot; i += 256) hot_w[i] = w[hot_lo + i];
-    __syncthreads();
-  }
 
   int64_t base = wave * RPI;
   int32_t raw[U][F];
@@ -93,12 +72,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
         bad |= id[u][f] != raw[u][f];
-        const char* src = E + (int64_t)id[u][f] * ROW_BYTES + sub * 16;
-        if constexpr (HOT) {   // branch-free: one flat load from LDS or the table
-          const char* l = reinterpret_cast<const char*>(&hot_rows[(id[u][f] - hot_lo) * LPR + sub]);
-          src = id[u][f] >= hot_lo ? l : src;
-        }
-        c[u][f].template load<NT>(src);
+        c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
     // Σ_f w[x_f]: lane `sub` gathers fields f ≡ sub (mod LPR); loads are
@@ -115,9 +89,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
           int32_t my = id[u][0];
 #pragma unroll
           for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
-          float wl;
-          if constexpr (HOT) wl = my >= hot_lo ? hot_w[my - hot_lo] : w[my];
-          else wl = w[my];
+          const float wl = w[my];
           wv[u] += (fsel < F) ? wl : 0.f;
         }
       }
@@ -313,28 +285,18 @@ static int grid_for(int64_t rows, int64_t rows_per_block) {
 template <int F, int LPR, bool BF16>
 static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            int64_t M, const float* w, float w0, float* out,
-                           bool nt, int32_t hot_lo, int32_t* status, hipStream_t s) {
+                           bool nt, int32_t* status, hipStream_t s) {
   constexpr int RPB = 4 * (kWave / LPR) * RowsPerLane<F>::value;
   const int grid = grid_for(B, RPB);
-  // hot tail staged when it fits and the workgroups have rows enough to pay
-  // for the staging copy (>= 32 each)
-  const bool hot = !nt && hot_lo < M && (M - hot_lo) * LPR * 16 <= kHotBytes &&
-                   M - hot_lo <= kHotRows && B >= (int64_t)grid * 32;
   if (w && nt)
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, true>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status, (int32_t)M);
-  else if (w && hot)
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, false, true>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status, hot_lo);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else if (w)
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, false>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status, (int32_t)M);
-  else if (hot)
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, false, true>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status, hot_lo);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else
     hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, false>), dim3(grid),
-                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status, (int32_t)M);
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
 }
 
 template <int F, int LPR, bool BF16>
@@ -374,11 +336,11 @@ static void launch_hybrid_fast(const int32_t* idx, int64_t B, int nctx,
 
 static bool try_fm_fast(const int32_t* idx, int64_t B, int F, const char* E,
                         int64_t M, int lpr, bool bf16, const float* w, float w0,
-                        float* out, bool nt, int32_t hot_lo, int32_t* status, hipStream_t s) {
+                        float* out, bool nt, int32_t* status, hipStream_t s) {
   if (bf16) {
-    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, nt, hot_lo, status, s)
+    HHFM_F_SWITCH(launch_fm_fast, true, idx, B, E, M, w, w0, out, nt, status, s)
   } else {
-    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, nt, hot_lo, status, s)
+    HHFM_F_SWITCH(launch_fm_fast, false, idx, B, E, M, w, w0, out, nt, status, s)
   }
   return true;
 }
@@ -407,8 +369,8 @@ using namespace hhfm;
 extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
                                      const void* E, int64_t features_M, int32_t k,
                                      int32_t dtype, const float* w, float w0,
-                                     float* out, int32_t flags, int64_t hot_begin,
-                                     int32_t* status, void* stream) {
+                                     float* out, int32_t flags, int32_t* status,
+                                     void* stream) {
   if (B < 0 || F < 1 || F > 64 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (dtype != HHFM_F32 && dtype != HHFM_BF16) return HHFM_EINVAL;
   if (flags & ~HHFM_FLAG_STREAM_TABLE) return HHFM_EINVAL;
@@ -420,10 +382,8 @@ extern "C" int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
   const bool aligned = (reinterpret_cast<uintptr_t>(E) & 15) == 0;
   if (!(lpr && aligned &&
         try_fm_fast(idx, B, F, reinterpret_cast<const char*>(E), features_M,
-                    lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0,
-                    (int32_t)(hot_begin > 0 && hot_begin < features_M ? hot_begin
-                                                                       : features_M),
-                    status, s))) {
+                    lpr, bf16, w, w0, out, (flags & HHFM_FLAG_STREAM_TABLE) != 0, status,
+                    s))) {
     const int grid = grid_for(B, 4);
     if (bf16)
       hipLaunchKernelGGL(fm_rows_generic<true>, dim3(grid), dim3(256), 0, s, idx,
@@ -442,7 +402,7 @@ extern "C" int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                                   int32_t dtype, const float* w, float w0,
                                   float* out, void* stream) {
   return hhfm_fm_score_rows_ex(idx, B, F, E, features_M, k, dtype, w, w0, out,
-                               HHFM_FM_ROWS_DEFAULT_FLAGS, features_M, nullptr, stream);
+                               HHFM_FM_ROWS_DEFAULT_FLAGS, nullptr, stream);
 }
 
 extern "C" int hhfm_hybrid_score_rows_ex(const int32_t* idx, int64_t B,

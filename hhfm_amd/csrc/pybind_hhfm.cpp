@@ -67,14 +67,13 @@ PYBIND11_MODULE(_hhfm, m) {
 
   m.def("fm_score_rows_ex",
         [](uptr idx, int64_t B, int F, uptr E, int64_t M, int k, int dtype,
-           uptr w, float w0, uptr out, int flags, int64_t hot_begin, uptr status,
-           uptr stream) {
+           uptr w, float w0, uptr out, int flags, uptr status, uptr stream) {
           int rc;
           {
             py::gil_scoped_release nogil;
             rc = hhfm_fm_score_rows_ex(P<const int32_t>(idx), B, F, P<const void>(E),
                                        M, k, dtype, P<const float>(w), w0,
-                                       P<float>(out), flags, hot_begin, P<int32_t>(status),
+                                       P<float>(out), flags, P<int32_t>(status),
                                        P<void>(stream));
           }
           check(rc, "hhfm_fm_score_rows_ex");

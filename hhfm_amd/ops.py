@@ -109,12 +109,9 @@ def _status_ptr(status: Optional[torch.Tensor]) -> int:
 
 def fm_score_rows(idx: torch.Tensor, E: torch.Tensor, w: Optional[torch.Tensor],
                   w0: float = 0.0, out: Optional[torch.Tensor] = None,
-                  status: Optional[torch.Tensor] = None, flags: int = 0,
-                  hot_begin: Optional[int] = None) -> torch.Tensor:
+                  status: Optional[torch.Tensor] = None, flags: int = 0) -> torch.Tensor:
     """FM.out (FM.py:99-120) for rows ``idx`` [B, F] -> float32 [B].
-    ``status``: optional device int32 word the kernel flags bad ids in;
-    ``hot_begin``: first row of the table's hot tail (the context vocabulary,
-    n_user + n_item in LoadData's numbering) — a staging hint, same bits."""
+    ``status``: optional device int32 word the kernel flags bad ids in."""
     _idx(idx, "idx")
     dev = _need_cuda(idx, E, w, out)
     B, F = idx.shape
@@ -125,8 +122,7 @@ def fm_score_rows(idx: torch.Tensor, E: torch.Tensor, w: Optional[torch.Tensor],
         out = torch.empty(B, dtype=torch.float32, device=dev)
     native().fm_score_rows_ex(idx.data_ptr(), B, F, E.data_ptr(), M, k, _dtype_code(E),
                               0 if w is None else w.data_ptr(), float(w0),
-                              out.data_ptr(), int(flags), M if hot_begin is None else int(hot_begin),
-                              _status_ptr(status), _stream(dev))
+                              out.data_ptr(), int(flags), _status_ptr(status), _stream(dev))
     return out
 
 

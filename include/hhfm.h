@@ -90,14 +90,10 @@ int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
                        int32_t dtype, const float* w, float w0, float* out,
                        void* stream);
 
-/* Same, with tuning flags, a hot-row hint and an optional id status word:
+/* Same, with tuning flags and an optional id status word:
  *   HHFM_FLAG_STREAM_TABLE — read embedding rows / ids and write `out` with
  *   non-temporal accesses (measured 10 % slower at configs[1]).
  *   Any other bit is rejected with HHFM_EINVAL.
- * hot_begin: rows [hot_begin, features_M) are read by most rows (LoadData's
- *   context vocabulary, NewLoadData.py:29-34: ids n_user + n_item ..): when
- *   they fit (<= 16 KiB, <= 256 rows) every workgroup stages them in LDS once.
- *   A hint only — any value gives the same bits; features_M (or <= 0) = none.
  * status: NULL, or a device int32 the kernel ORs HHFM_STATUS_BAD_ID into when
  *   it meets an id outside [0, features_M) (such ids are read as row 0 so the
  *   kernel cannot fault).  hhfm_status_read() turns it into HHFM_EINVAL —
@@ -108,7 +104,7 @@ int hhfm_fm_score_rows(const int32_t* idx, int64_t B, int32_t F,
 int hhfm_fm_score_rows_ex(const int32_t* idx, int64_t B, int32_t F,
                           const void* E, int64_t features_M, int32_t k,
                           int32_t dtype, const float* w, float w0, float* out,
-                          int32_t flags, int64_t hot_begin, int32_t* status, void* stream);
+                          int32_t flags, int32_t* status, void* stream);
 
 /* ------------------------------------------------------------------------
  * H1 — HHFM per-row score (replaces `OUR.PositiveFeadback`,

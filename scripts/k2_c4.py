@@ -62,8 +62,10 @@ def main():
             else:
                 same = bool(torch.equal(i, ref[1]) and torch.equal(s, ref[0]))
             ms = float(np.median(ts))
+            import hashlib
+            sha = hashlib.sha256(i.cpu().numpy().tobytes() + s.cpu().numpy().tobytes()).hexdigest()
             res[f"{tname}_{var}"] = {"ms": ms, "TFLOPs": 2.0 * k * B * N / (ms * 1e-3) / 1e12,
-                                     "ids_equal_first_variant": same}
+                                     "ids_equal_first_variant": same, "sha16": sha[:16]}
             print(json.dumps({f"{tname}_{var}": res[f"{tname}_{var}"]}), flush=True)
     print(json.dumps(res))
 

@@ -77,9 +77,9 @@ def test_plan_and_flag_bits_validated_without_device():
     lib = ctypes.CDLL(LIB)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     lib.hhfm_fm_score_rows_ex.argtypes = [vp, i64, i32, vp, i64, i32, i32, vp, ctypes.c_float,
-                                          vp, i32, i64, vp, vp]
+                                          vp, i32, vp, vp]
     assert lib.hhfm_fm_score_rows_ex(None, 10, 5, None, 10, 64, 0, None, 0.0, None, 1 << 4,
-                                     10, None, None) == -1
+                                     None, None) == -1
     lib.hhfm_topk_dense_ex.argtypes = [vp, i64, i32, i64, i32, i32, vp, vp, i32, vp]
     assert lib.hhfm_topk_dense_ex(None, 4, 100, 100, 5, 0, None, None, 1 << 11, None) == -1
     assert lib.hhfm_topk_dense_ex(None, 0, 100, 100, 5, 0, None, None, 1 << 10, None) == 0
@@ -146,7 +146,7 @@ def test_bad_ids_reach_c_callers_as_einval():
     lib = ctypes.CDLL(LIB)
     vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32
     lib.hhfm_fm_score_rows_ex.argtypes = [vp, i64, i32, vp, i64, i32, i32, vp, ctypes.c_float,
-                                          vp, i32, i64, vp, vp]
+                                          vp, i32, vp, vp]
     lib.hhfm_hybrid_score_rows_ex.argtypes = [vp, i64, i32, i32, i32, i32, i32, i32, i32, vp,
                                               i64, i32, i32, vp, vp, vp]
     lib.hhfm_status_read.argtypes = [vp, vp]
@@ -165,7 +165,7 @@ def test_bad_ids_reach_c_callers_as_einval():
             for fn in ("fm", "hybrid"):
                 if fn == "fm":
                     rc = lib.hhfm_fm_score_rows_ex(X.data_ptr(), 4097, 5, Ek.data_ptr(), M, kk, 0,
-                                                   w.data_ptr(), 0.0, out.data_ptr(), 0, M - 12,
+                                                   w.data_ptr(), 0.0, out.data_ptr(), 0,
                                                    st.data_ptr(), stream)
                 else:
                     rc = lib.hhfm_hybrid_score_rows_ex(X.data_ptr(), 4097, 5, 0, 1, 2, 5, 0, 0,
@@ -175,7 +175,7 @@ def test_bad_ids_reach_c_callers_as_einval():
                 assert lib.hhfm_status_read(st.data_ptr(), stream) == -1, (bad_value, kk, fn)
                 # the word is cleared by the read; a clean batch reports OK
                 lib.hhfm_fm_score_rows_ex(good.data_ptr(), 4097, 5, Ek.data_ptr(), M, kk, 0,
-                                          w.data_ptr(), 0.0, out.data_ptr(), 0, M, st.data_ptr(),
+                                          w.data_ptr(), 0.0, out.data_ptr(), 0, st.data_ptr(),
                                           stream)
                 assert lib.hhfm_status_read(st.data_ptr(), stream) == 0
     # catalog: a bad context id in a query row

@@ -108,49 +108,10 @@ def test_fm_score_rows_flag_variants_bit_identical(dtype, k, F):
         o = torch.full((B,), float("nan"), device="cuda")
         native().fm_score_rows_ex(X.data_ptr(), B, F, E.data_ptr(), M, k,
                                   1 if dtype == "bf16" else 0, w.data_ptr(), 0.003,
-                                  o.data_ptr(), flags, M, 0, st)
+                                  o.data_ptr(), flags, 0, st)
         outs.append(o.cpu())
     for o in outs[1:]:
         assert torch.equal(o, outs[0])
-
-
-@pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("k,F,tail", [(64, 5, 12), (64, 5, 64), (32, 3, 100), (128, 8, 30),
-                                      (16, 12, 256)])
-def test_fm_score_rows_hot_tail(dtype, k, F, tail):
-    """The hot-tail staging (hot_begin: the last `tail` table rows — LoadData's
-    context vocabulary — staged in LDS per workgroup) gives the bits of the
-    unstaged kernel: fields whose ids are all in the tail (the context
-    columns), mixed waves (user / item columns with ids drawn over the whole
-    table, tail included), bad ids flagged the same way; and the oracle's
-    values (1e-5 relative, κ <= 100)."""
-    from hhfm_amd import ops
-    rng = np.random.default_rng(31 * k + F + tail)
-    B, M = 300_000, 60_000
-    X = rng.integers(0, M, size=(B, F)).astype(np.int32)
-    X[:, 2:] = rng.integers(M - min(tail, 12), M, size=(B, F - 2))   # context columns
-    X[:1000, 0] = rng.integers(M - tail, M, 1000)                     # hot users (mixed waves)
-    E = table(rng, M, k)
-    w = rng.normal(0, 0.01, size=M).astype(np.float32)
-    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
-    if dtype == "bf16":
-        E = bf16_round(E)
-    Xd = _dev(X)
-    plain = ops.fm_score_rows(Xd, Eg, _dev(w), 0.003).cpu()
-    st = torch.zeros(1, dtype=torch.int32, device="cuda")
-    hot = ops.fm_score_rows(Xd, Eg, _dev(w), 0.003, hot_begin=M - tail, status=st).cpu()
-    assert int(st.item()) == 0
-    assert torch.equal(plain, hot)
-    nw = ops.fm_score_rows(Xd, Eg, None, 0.0, hot_begin=M - tail).cpu()
-    assert torch.equal(nw, ops.fm_score_rows(Xd, Eg, None, 0.0).cpu())
-    got = hot.numpy()
-    ref = orc.fm_out(X[:20000], E, w, 0.003)[:, 0]
-    _elementwise_vs_exact(got[:20000], ref, X[:20000], E, w, 0.003,
-                          _fm_scale(X[:20000], E, w, 0.003))
-    Xb = X.copy()
-    Xb[123_456, F - 1] = M + 7                                        # a bad context id
-    ops.fm_score_rows(_dev(Xb), Eg, _dev(w), 0.003, hot_begin=M - tail, status=st)
-    assert int(st.item()) != 0
 
 
 @pytest.mark.parametrize("B", [0, 1, 7, 63, 1000])
