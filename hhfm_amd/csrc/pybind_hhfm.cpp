@@ -402,8 +402,8 @@ PYBIND11_MODULE(_hhfm, m) {
            size_t ws_bytes, uptr loss, uptr stream) {
           if (W.size() != dims.size() || bias.size() != dims.size())
             throw py::value_error("dims, W and bias must have the same length");
-          if (opt == 0 && acc.size() != 2 * dims.size() + 4)
-            throw py::value_error("acc needs 2 * len(dims) + 4 accumulators");
+          if (opt != 1 && acc.size() != 2 * dims.size() + 4)
+            throw py::value_error("acc needs 2 * len(dims) + 4 slot arrays");
           std::vector<float*> Wv(W.size()), bv(bias.size()), av(acc.size());
           for (size_t i = 0; i < W.size(); ++i) {
             Wv[i] = P<float>(W[i]);
@@ -432,8 +432,8 @@ PYBIND11_MODULE(_hhfm, m) {
         [](uptr idx, uptr y, int64_t B, int F, uptr E, uptr w, uptr w0, int64_t M, int k, int A,
            uptr W, uptr b, uptr pvec, uptr Pv, float lr, float lam, int opt,
            std::vector<uptr> acc, uptr ws, size_t ws_bytes, uptr loss, uptr stream) {
-          if (opt == 0 && acc.size() != 7)
-            throw py::value_error("acc needs 7 accumulators (E, w, w0, W, b, pvec, P)");
+          if (opt != 1 && acc.size() != 7)
+            throw py::value_error("acc needs 7 slot arrays (E, w, w0, W, b, pvec, P)");
           std::vector<float*> av(acc.size());
           for (size_t i = 0; i < acc.size(); ++i) av[i] = P<float>(acc[i]);
           int rc;

@@ -14,10 +14,11 @@
 // atomics (the embedding gradient is a scatter by nature; rows repeat).  The
 // L2 term λ·Σ E²/2 (tf.contrib.layers.l2_regularizer) makes the embedding
 // gradient dense, so — exactly like TF — the optimizer then updates the whole
-// table: `optimizer_dense` applies TF's ApplyAdagrad (accum += g², var -= lr·
-// g·rsqrt(accum), accumulators initialised to 0.1 by the caller) or plain
-// gradient descent, and accumulates Σ var² of the pre-update table for the
-// reported loss (TF evaluates `loss` and the update in the same run).
+// table: `optimizer_apply` applies TF's Adagrad (accumulators initialised to
+// 0.1 by the caller), GradientDescent, Momentum or Adam (slots initialised to
+// 0) with the sparse-gradient rules TF uses for IndexedSlices variables, and
+// accumulates Σ var² of the pre-update table for the reported loss (TF
+// evaluates `loss` and the update in the same run).
 // Gradients of reduce_max split equally between tied maxima (TF _MaxGrad).
 #include "gemm_mfma.h"
 
@@ -27,6 +28,7 @@ enum { OPT_ADAGRAD = 0, OPT_SGD = 1 };
 constexpr int kMaxNeg = 16;   // negatives per row (the reference samples 10, OurModel7.py:371)
 
 // scal[0] = Σ dL/d(w0)  scal[1] = data loss  scal[2] = Σ E² (pre-update)  scal[3] = Σ w² (unused)
+// scal[8], scal[9] = Adam's β1^t, β2^t (kept between steps; 0 = not started)
 __global__ __launch_bounds__(256) void fm_train_rows(
     const int32_t* __restrict__ idx, const float* __restrict__ y, int64_t B, int F,
     const float* __restrict__ E, const float* __restrict__ w, const float* __restrict__ w0,
@@ -140,25 +142,74 @@ __global__ __launch_bounds__(256) void hhfm_train_rows(
   }
 }
 
-// var -= lr·g·rsqrt(accum += g²) (Adagrad) or var -= lr·g (SGD);
+// One TF-1.x optimizer step on a variable (training_ops.cc semantics, fp32):
+//   Adagrad   accum += g²; var -= lr·g·rsqrt(accum)           (ApplyAdagrad)
+//   SGD       var -= lr·g                                      (ApplyGradientDescent)
+//   Momentum  accum = accum·0.95 + g; var -= accum·lr           (ApplyMomentum,
+//             momentum 0.95 as FM.py:136); a SPARSE variable (its gradient an
+//             IndexedSlices: embedding_lookup without a dense l2 term) updates
+//             only the rows the batch touched (SparseApplyMomentum)
+//   Adam      β1 0.9, β2 0.999, ε 1e-8 (FM.py:130), α = lr·√(1−β2^t)/(1−β1^t):
+//             dense  m += (g−m)(1−β1); v += (g²−v)(1−β2); var -= m·α/(√v+ε)
+//             (ApplyAdam); sparse (AdamOptimizer._apply_sparse_shared)
+//             m = m·β1 + g(1−β1); v = v·β2 + g²(1−β2) on every row, the same
+//             var update — the two differ only in rounding
 // g = grad + λ·var; Σ var² (pre-update) accumulated into *sumsq when given.
-__global__ __launch_bounds__(256) void optimizer_dense(float* __restrict__ var,
+// state: Adagrad / Momentum n floats, Adam 2n (m, then v).  pw: the step's
+// β1^t, β2^t (TF's beta1_power / beta2_power; 0 = the first step: β1, β2).
+enum { OPT_MOMENTUM = 2, OPT_ADAM = 3 };
+constexpr float kMomentum = 0.95f, kBeta1 = 0.9f, kBeta2 = 0.999f, kAdamEps = 1e-8f;
+
+struct OptStep {
+  int opt;
+  float lr;
+  const float* pw;         // Adam: [β1^t, β2^t] (device)
+  const uint8_t* touched;  // sparse Momentum: rows the batch touched (else null)
+  int rowlen;              // elements per row of the variable (touched index = i / rowlen)
+  int sparse;              // the variable's TF gradient is an IndexedSlices
+};
+
+__global__ __launch_bounds__(256) void optimizer_apply(float* __restrict__ var,
                                                        float* __restrict__ grad,
-                                                       float* __restrict__ accum, int64_t n,
-                                                       float lr, float lam, int opt,
+                                                       float* __restrict__ state, int64_t n,
+                                                       float lam, OptStep o,
                                                        float* __restrict__ sumsq) {
+  float alpha = 0.f;
+  if (o.opt == OPT_ADAM) {
+    const float b1p = o.pw[0] != 0.f ? o.pw[0] : kBeta1;
+    const float b2p = o.pw[1] != 0.f ? o.pw[1] : kBeta2;
+    alpha = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  }
   float ss = 0.f;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const float v = var[i];
     ss += v * v;
     const float g = grad[i] + lam * v;
-    if (opt == OPT_ADAGRAD) {
-      const float a = accum[i] + g * g;
-      accum[i] = a;
-      var[i] = v - lr * g * rsqrtf(a);
+    if (o.opt == OPT_ADAGRAD) {
+      const float a = state[i] + g * g;
+      state[i] = a;
+      var[i] = v - o.lr * g * rsqrtf(a);
+    } else if (o.opt == OPT_SGD) {
+      var[i] = v - o.lr * g;
+    } else if (o.opt == OPT_MOMENTUM) {
+      if (!o.sparse || o.touched[i / o.rowlen]) {
+        const float a = state[i] * kMomentum + g;
+        state[i] = a;
+        var[i] = v - a * o.lr;
+      }
     } else {
-      var[i] = v - lr * g;
+      float m = state[i], vv = state[n + i];
+      if (o.sparse) {
+        m = m * kBeta1 + g * (1.f - kBeta1);
+        vv = vv * kBeta2 + (g * g) * (1.f - kBeta2);
+      } else {
+        m += (g - m) * (1.f - kBeta1);
+        vv += (g * g - vv) * (1.f - kBeta2);
+      }
+      state[i] = m;
+      state[n + i] = vv;
+      var[i] = v - (m * alpha) / (sqrtf(vv) + kAdamEps);
     }
     grad[i] = 0.f;   // leave the gradient buffer zeroed for the next step
   }
@@ -168,15 +219,20 @@ __global__ __launch_bounds__(256) void optimizer_dense(float* __restrict__ var,
   }
 }
 
-__global__ void fm_bias_update(float* w0, float* acc0, float* scal, float lr, int opt) {
-  const float g = scal[0];
-  if (opt == OPT_ADAGRAD) {
-    const float a = acc0[0] + g * g;
-    acc0[0] = a;
-    w0[0] = w0[0] - lr * g * rsqrtf(a);
-  } else {
-    w0[0] = w0[0] - lr * g;
-  }
+// after every variable's update: β1^t, β2^t -> β1^(t+1), β2^(t+1) (AdamOptimizer._finish)
+__global__ void adam_advance(float* pw) {
+  pw[0] = (pw[0] != 0.f ? pw[0] : kBeta1) * kBeta1;
+  pw[1] = (pw[1] != 0.f ? pw[1] : kBeta2) * kBeta2;
+}
+
+// touched[x] = val for every id of the batch (rows of a sparse variable the
+// step updates under Momentum); plain byte stores, equal values
+__global__ __launch_bounds__(256) void mark_rows(const int32_t* __restrict__ idx, int64_t n,
+                                                 int64_t M, uint8_t* __restrict__ touched,
+                                                 uint8_t val) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    touched[clamp_id(idx[i], M)] = val;
 }
 
 __global__ void finish_loss(float* scal, float lam, float* loss) {
@@ -187,6 +243,20 @@ __global__ void finish_loss(float* scal, float lam, float* loss) {
 static int grid_for_n(int64_t n) {
   int64_t g = (n + 255) / 256;
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+static bool opt_ok(int opt) {
+  return opt == OPT_ADAGRAD || opt == OPT_SGD || opt == OPT_MOMENTUM || opt == OPT_ADAM;
+}
+
+// one optimizer_apply launch; `sparse` variables under Momentum need the
+// touched mask (`mark_rows` before, cleared after by the caller)
+static void apply_opt(float* var, float* grad, float* state, int64_t n, float lam, int opt,
+                      float lr, const float* pw, const uint8_t* touched, int rowlen, bool sparse,
+                      float* sumsq, hipStream_t st) {
+  OptStep o{opt, lr, pw, touched, rowlen > 0 ? rowlen : 1, sparse ? 1 : 0};
+  hipLaunchKernelGGL(optimizer_apply, dim3(grid_for_n(n)), dim3(256), 0, st, var, grad, state, n,
+                     lam, o, sumsq);
 }
 
 // ---------------------------------------------------------------------------
@@ -390,7 +460,7 @@ struct DfmTrainPlan {
   int64_t off_dW[kDfmTrainMaxLayers], off_db[kDfmTrainMaxLayers];
   int64_t off_H[kDfmTrainMaxLayers + 1], off_HT[kDfmTrainMaxLayers];
   int64_t off_G[kDfmTrainMaxLayers + 1], off_GT[kDfmTrainMaxLayers + 1];
-  int64_t off_dX0, off_g, off_dWp, off_dE, off_dw, off_scal;
+  int64_t off_dX0, off_g, off_dWp, off_dE, off_dw, off_scal, off_touch;
   int64_t total;   // floats
 };
 
@@ -409,6 +479,13 @@ static bool dfm_train_plan(int64_t B, int F, int k, int64_t M, int L, const int3
   p.Bp = pad8(B > 0 ? B : 1);
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  // zero-initialised, kept zeroed by the step (scalars incl. Adam's β powers,
+  // dE, dw, touched mask): first, at B-independent offsets, so a workspace
+  // grown for a larger batch keeps its state by copying the old one's bytes
+  p.off_scal = take(16);
+  p.off_dE = take(M * k);
+  p.off_dw = take(M);
+  p.off_touch = take((M + 3) / 4);   // touched-row mask, M bytes
   for (int i = 0; i < L; ++i) {
     p.off_WtP[i] = take((int64_t)p.d[i + 1] * pad8(p.d[i]));
     p.off_WP[i] = take((int64_t)p.d[i] * pad8(p.d[i + 1]));
@@ -424,10 +501,6 @@ static bool dfm_train_plan(int64_t B, int F, int k, int64_t M, int L, const int3
   p.off_dX0 = take(p.Bp * p.D0);
   p.off_g = take(p.Bp);
   p.off_dWp = take(F + k + p.d[L]);
-  // zero-initialised, kept zeroed by the step: dE, dw, scalars
-  p.off_dE = take(M * k);
-  p.off_dw = take(M);
-  p.off_scal = take(16);
   p.total = o;
   return true;
 }
@@ -659,7 +732,7 @@ struct AfmTrainPlan {
   int64_t n, Kp;
   int S;
   int64_t off_Wt, off_R, off_Gz, off_T, off_DP, off_att, off_g, off_part;
-  int64_t off_dE, off_dw, off_dW, off_db, off_dpv, off_dP, off_scal;
+  int64_t off_dE, off_dw, off_dW, off_db, off_dpv, off_dP, off_scal, off_touch;
   int64_t total;   // floats
 };
 
@@ -675,6 +748,16 @@ static bool afm_train_plan(int64_t B, int F, int k, int A, int64_t M, AfmTrainPl
   p.S = (int)((p.Kp + kAfmSplitK - 1) / kAfmSplitK);
   int64_t o = 0;
   auto take = [&](int64_t n) { const int64_t r = o; o += (n + 63) & ~int64_t(63); return r; };
+  // zero-initialised, kept zeroed by the step; first, at B-independent
+  // offsets (see dfm_train_plan)
+  p.off_scal = take(16);
+  p.off_dE = take(M * k);
+  p.off_dw = take(M);
+  p.off_dW = take((int64_t)k * A);
+  p.off_db = take(A);
+  p.off_dpv = take(A);
+  p.off_dP = take(k);
+  p.off_touch = take((M + 3) / 4);   // touched-row mask, M bytes
   p.off_Wt = take((int64_t)A * k);
   p.off_R = take(p.n * A);
   p.off_Gz = take(p.n * A);
@@ -683,14 +766,6 @@ static bool afm_train_plan(int64_t B, int F, int k, int A, int64_t M, AfmTrainPl
   p.off_att = take(p.n);
   p.off_g = take(B);
   p.off_part = take((int64_t)p.S * k * A);
-  // zero-initialised, kept zeroed by the step
-  p.off_dE = take(M * k);
-  p.off_dw = take(M);
-  p.off_dW = take((int64_t)k * A);
-  p.off_db = take(A);
-  p.off_dpv = take(A);
-  p.off_dP = take(k);
-  p.off_scal = take(16);
   p.total = o;
   return true;
 }
@@ -700,8 +775,10 @@ static bool afm_train_plan(int64_t B, int F, int k, int A, int64_t M, AfmTrainPl
 using namespace hhfm;
 
 extern "C" size_t hhfm_train_workspace(int64_t features_M, int32_t k) {
-  // dE [M*k] + dw [M] + 4 scalars; must be zero-filled once by the caller
-  return (size_t)features_M * k * 4 + (size_t)features_M * 4 + 64;
+  // dE [M*k] + dw [M] + 16 scalars + the touched-row mask [M] bytes; must be
+  // zero-filled once by the caller
+  return (size_t)features_M * k * 4 + (size_t)features_M * 4 + 64 +
+         (((size_t)features_M + 255) & ~size_t(255));
 }
 
 extern "C" int hhfm_fm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F,
@@ -710,23 +787,32 @@ extern "C" int hhfm_fm_train_step(const int32_t* idx, const float* y, int64_t B,
                                   float* accw, float* accw0, void* workspace, size_t ws_bytes,
                                   float* loss, void* stream) {
   if (B < 0 || F < 1 || k < 1 || features_M < 1) return HHFM_EINVAL;
-  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!opt_ok(optimizer)) return HHFM_EUNSUPPORTED;
   if (!idx || !y || !E || !w || !w0 || !loss || !workspace) return HHFM_EINVAL;
-  if (optimizer == OPT_ADAGRAD && (!accE || !accw || !accw0)) return HHFM_EINVAL;
+  if (optimizer != OPT_SGD && (!accE || !accw || !accw0)) return HHFM_EINVAL;
   if (ws_bytes < hhfm_train_workspace(features_M, k)) return HHFM_EWORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* dE = reinterpret_cast<float*>(workspace);
   float* dw = dE + features_M * k;
   float* scal = dw + features_M;
+  uint8_t* touched = reinterpret_cast<uint8_t*>(scal + 16);
   if (B > 0)
     hipLaunchKernelGGL(fm_train_rows, dim3(grid_for_n(B * 64)), dim3(256), 0, st, idx, y, B, F,
                        E, w, w0, features_M, k, dE, dw, scal);
+  // sparse gradients (FM.py:123-126): w's always (embedding_lookup only), E's
+  // when λ = 0 (no dense l2 term); w0 and the λ > 0 table are dense
+  const bool mark = optimizer == OPT_MOMENTUM && B > 0;
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)1);
   const int64_t nE = features_M * k;
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, dE, accE, nE,
-                     lr, lam, optimizer, scal + 2);
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(features_M)), dim3(256), 0, st, w, dw,
-                     accw, features_M, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, w0, accw0, scal, lr, optimizer);
+  apply_opt(E, dE, accE, nE, lam, optimizer, lr, scal + 8, touched, k, lam == 0.f, scal + 2, st);
+  apply_opt(w, dw, accw, features_M, 0.f, optimizer, lr, scal + 8, touched, 1, true, nullptr, st);
+  apply_opt(w0, scal, accw0, 1, 0.f, optimizer, lr, scal + 8, nullptr, 1, false, nullptr, st);
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)0);
+  if (optimizer == OPT_ADAM) hipLaunchKernelGGL(adam_advance, dim3(1), dim3(1), 0, st, scal + 8);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lam, loss);
   return (int)hipGetLastError();
 }
@@ -739,20 +825,36 @@ extern "C" int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_
                                     size_t ws_bytes, float* loss, void* stream) {
   if (B < 0 || ncols < 2 || NG < 1 || k < 1 || features_M < 1) return HHFM_EINVAL;
   if (NG > kMaxNeg) return HHFM_EUNSUPPORTED;
-  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!opt_ok(optimizer)) return HHFM_EUNSUPPORTED;
   if (!X || !Neg || !E || !loss || !workspace) return HHFM_EINVAL;
-  if (optimizer == OPT_ADAGRAD && !accE) return HHFM_EINVAL;
+  if (optimizer != OPT_SGD && !accE) return HHFM_EINVAL;
   if (ws_bytes < hhfm_train_workspace(features_M, k)) return HHFM_EWORKSPACE;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   float* dE = reinterpret_cast<float*>(workspace);
   float* scal = dE + features_M * k + features_M;
+  uint8_t* touched = reinterpret_cast<uint8_t*>(scal + 16);
   if (B > 0)
     hipLaunchKernelGGL(hhfm_train_rows, dim3(grid_for_n(B * 64)), dim3(256), 0, st, X, Neg, B,
                        ncols, ctx_begin, ctx_end, time_begin, time_end, NG, E, features_M, k,
                        dE, scal);
+  // E's gradient is dense through λ·l2(E) (OurModel7.py:180-184), sparse at λ = 0
+  const bool sparseE = lam == 0.f;
+  const bool mark = optimizer == OPT_MOMENTUM && sparseE && B > 0;
+  if (mark) {
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * ncols)), dim3(256), 0, st, X, B * ncols,
+                       features_M, touched, (uint8_t)1);
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * NG)), dim3(256), 0, st, Neg, B * NG,
+                       features_M, touched, (uint8_t)1);
+  }
   const int64_t nE = features_M * k;
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, dE, accE, nE,
-                     lr, lam, optimizer, scal + 2);
+  apply_opt(E, dE, accE, nE, lam, optimizer, lr, scal + 8, touched, k, sparseE, scal + 2, st);
+  if (mark) {
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * ncols)), dim3(256), 0, st, X, B * ncols,
+                       features_M, touched, (uint8_t)0);
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * NG)), dim3(256), 0, st, Neg, B * NG,
+                       features_M, touched, (uint8_t)0);
+  }
+  if (optimizer == OPT_ADAM) hipLaunchKernelGGL(adam_advance, dim3(1), dim3(1), 0, st, scal + 8);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lam, loss);
   return (int)hipGetLastError();
 }
@@ -779,13 +881,13 @@ extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B
   if (B < 0 || features_M < 1 || !layer_dims ||
       !dfm_train_plan(B, F, k, features_M, nlayers, layer_dims, p))
     return HHFM_EINVAL;
-  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!opt_ok(optimizer)) return HHFM_EUNSUPPORTED;
   if (!idx || !y || !E || !w || !W || !bias || !Wp || !bp || !loss || !workspace)
     return HHFM_EINVAL;
   const int L = p.L;
   for (int i = 0; i < L; ++i)
     if (!W[i] || !bias[i]) return HHFM_EINVAL;
-  if (optimizer == OPT_ADAGRAD) {   // acc: E, w, W_0..W_{L-1}, b_0..b_{L-1}, Wp, bp
+  if (optimizer != OPT_SGD) {   // acc: E, w, W_0..W_{L-1}, b_0..b_{L-1}, Wp, bp
     if (!acc) return HHFM_EINVAL;
     for (int i = 0; i < 2 * L + 4; ++i)
       if (!acc[i]) return HHFM_EINVAL;
@@ -797,7 +899,8 @@ extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B
   float* scal = at(p.off_scal);
   const int64_t Bp = p.Bp;
   const int64_t nE = features_M * k;
-  auto acc_of = [&](int i) { return optimizer == OPT_ADAGRAD ? acc[i] : (float*)nullptr; };
+  auto acc_of = [&](int i) { return optimizer != OPT_SGD ? acc[i] : (float*)nullptr; };
+  uint8_t* touched = reinterpret_cast<uint8_t*>(at(p.off_touch));
 
   if (B > 0) {
     // weights: Wᵀ zero-padded (forward Bt) and W zero-padded (backward Bt)
@@ -890,28 +993,37 @@ extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B
     hipLaunchKernelGGL(dfm_train_scatter, dim3(grid_for_n(B * 64)), dim3(256), 0, st, idx, B, F,
                        E, features_M, k, at(p.off_dX0), at(p.off_g), Wp, at(p.off_dE));
   }
-  // optimizer: λ only on the layer weights and the concat projection (DFM.py:146-152)
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, at(p.off_dE),
-                     acc_of(0), nE, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(features_M)), dim3(256), 0, st, w,
-                     at(p.off_dw), acc_of(1), features_M, lr, 0.f, optimizer, (float*)nullptr);
+  // optimizer: λ only on the layer weights and the concat projection
+  // (DFM.py:146-152); the table and w have IndexedSlices gradients (sparse)
+  const bool mark = optimizer == OPT_MOMENTUM && B > 0;
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)1);
+  const float* pw = scal + 8;
+  apply_opt(E, at(p.off_dE), acc_of(0), nE, 0.f, optimizer, lr, pw, touched, k, true, nullptr,
+            st);
+  apply_opt(w, at(p.off_dw), acc_of(1), features_M, 0.f, optimizer, lr, pw, touched, 1, true,
+            nullptr, st);
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)0);
   for (int i = 0; i < L; ++i) {
     const int64_t n = (int64_t)p.d[i] * p.d[i + 1];
     if (B == 0) {
       (void)hipMemsetAsync(at(p.off_dW[i]), 0, n * 4, st);
       (void)hipMemsetAsync(at(p.off_db[i]), 0, p.d[i + 1] * 4, st);
     }
-    hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(n)), dim3(256), 0, st, W[i],
-                       at(p.off_dW[i]), acc_of(2 + i), n, lr, lambda_l2, optimizer, scal + 2);
-    hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(p.d[i + 1])), dim3(256), 0, st, bias[i],
-                       at(p.off_db[i]), acc_of(2 + L + i), (int64_t)p.d[i + 1], lr, 0.f,
-                       optimizer, (float*)nullptr);
+    apply_opt(W[i], at(p.off_dW[i]), acc_of(2 + i), n, lambda_l2, optimizer, lr, pw, nullptr, 1,
+              false, scal + 2, st);
+    apply_opt(bias[i], at(p.off_db[i]), acc_of(2 + L + i), (int64_t)p.d[i + 1], 0.f, optimizer,
+              lr, pw, nullptr, 1, false, nullptr, st);
   }
   const int64_t nWp = F + k + p.d[L];
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nWp)), dim3(256), 0, st, Wp, at(p.off_dWp),
-                     acc_of(2 + 2 * L), nWp, lr, lambda_l2, optimizer, scal + 2);
-  hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, bp, acc_of(3 + 2 * L), scal, lr,
-                     optimizer);
+  apply_opt(Wp, at(p.off_dWp), acc_of(2 + 2 * L), nWp, lambda_l2, optimizer, lr, pw, nullptr, 1,
+            false, scal + 2, st);
+  apply_opt(bp, scal, acc_of(3 + 2 * L), 1, 0.f, optimizer, lr, pw, nullptr, 1, false, nullptr,
+            st);
+  if (optimizer == OPT_ADAM) hipLaunchKernelGGL(adam_advance, dim3(1), dim3(1), 0, st, scal + 8);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lambda_l2, loss);
   return (int)hipGetLastError();
 }
@@ -932,10 +1044,10 @@ extern "C" int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B
                                    float* loss, void* stream) {
   AfmTrainPlan p;
   if (!afm_train_plan(B, F, k, A, features_M, p)) return HHFM_EINVAL;
-  if (optimizer != OPT_ADAGRAD && optimizer != OPT_SGD) return HHFM_EUNSUPPORTED;
+  if (!opt_ok(optimizer)) return HHFM_EUNSUPPORTED;
   if (!idx || !y || !E || !w || !w0 || !W || !b || !pvec || !P || !loss || !workspace)
     return HHFM_EINVAL;
-  if (optimizer == OPT_ADAGRAD) {   // acc: E, w, w0, W, b, pvec, P
+  if (optimizer != OPT_SGD) {   // acc: E, w, w0, W, b, pvec, P
     if (!acc) return HHFM_EINVAL;
     for (int i = 0; i < 7; ++i)
       if (!acc[i]) return HHFM_EINVAL;
@@ -947,7 +1059,8 @@ extern "C" int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B
   float* scal = at(p.off_scal);
   float* PT = at(p.off_T);
   float* GzT = PT + (int64_t)k * p.Kp;
-  auto acc_of = [&](int i) { return optimizer == OPT_ADAGRAD ? acc[i] : (float*)nullptr; };
+  auto acc_of = [&](int i) { return optimizer != OPT_SGD ? acc[i] : (float*)nullptr; };
+  uint8_t* touched = reinterpret_cast<uint8_t*>(at(p.off_touch));
 
   if (B > 0) {
     // Wᵀ [A][k] for the forward GEMM
@@ -1017,21 +1130,31 @@ extern "C" int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B
                        E, features_M, k, at(p.off_DP), at(p.off_att), at(p.off_g), P,
                        at(p.off_dE));
   }
+  // the table and w have IndexedSlices gradients (sparse); l2_regularizer(λ)
+  // on attention_W only (AFM.py:146)
+  const bool mark = optimizer == OPT_MOMENTUM && B > 0;
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)1);
+  const float* pw = scal + 8;
   const int64_t nE = features_M * k;
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(nE)), dim3(256), 0, st, E, at(p.off_dE),
-                     acc_of(0), nE, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n(features_M)), dim3(256), 0, st, w,
-                     at(p.off_dw), acc_of(1), features_M, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(fm_bias_update, dim3(1), dim3(1), 0, st, w0, acc_of(2), scal, lr, optimizer);
-  // l2_regularizer(λ)(attention_W) only (AFM.py:146)
-  hipLaunchKernelGGL(optimizer_dense, dim3(grid_for_n((int64_t)k * A)), dim3(256), 0, st, W,
-                     at(p.off_dW), acc_of(3), (int64_t)k * A, lr, lambda_att, optimizer, scal + 2);
-  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, b, at(p.off_db), acc_of(4),
-                     (int64_t)A, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, pvec, at(p.off_dpv), acc_of(5),
-                     (int64_t)A, lr, 0.f, optimizer, (float*)nullptr);
-  hipLaunchKernelGGL(optimizer_dense, dim3(1), dim3(256), 0, st, P, at(p.off_dP), acc_of(6),
-                     (int64_t)k, lr, 0.f, optimizer, (float*)nullptr);
+  apply_opt(E, at(p.off_dE), acc_of(0), nE, 0.f, optimizer, lr, pw, touched, k, true, nullptr,
+            st);
+  apply_opt(w, at(p.off_dw), acc_of(1), features_M, 0.f, optimizer, lr, pw, touched, 1, true,
+            nullptr, st);
+  if (mark)
+    hipLaunchKernelGGL(mark_rows, dim3(grid_for_n(B * F)), dim3(256), 0, st, idx, B * F,
+                       features_M, touched, (uint8_t)0);
+  apply_opt(w0, scal, acc_of(2), 1, 0.f, optimizer, lr, pw, nullptr, 1, false, nullptr, st);
+  apply_opt(W, at(p.off_dW), acc_of(3), (int64_t)k * A, lambda_att, optimizer, lr, pw, nullptr, 1,
+            false, scal + 2, st);
+  apply_opt(b, at(p.off_db), acc_of(4), (int64_t)A, 0.f, optimizer, lr, pw, nullptr, 1, false,
+            nullptr, st);
+  apply_opt(pvec, at(p.off_dpv), acc_of(5), (int64_t)A, 0.f, optimizer, lr, pw, nullptr, 1, false,
+            nullptr, st);
+  apply_opt(P, at(p.off_dP), acc_of(6), (int64_t)k, 0.f, optimizer, lr, pw, nullptr, 1, false,
+            nullptr, st);
+  if (optimizer == OPT_ADAM) hipLaunchKernelGGL(adam_advance, dim3(1), dim3(1), 0, st, scal + 8);
   hipLaunchKernelGGL(finish_loss, dim3(1), dim3(1), 0, st, scal, lambda_att, loss);
   return (int)hipGetLastError();
 }

@@ -21,25 +21,45 @@ from . import ops
 from .harness import partition_all
 from ._native import native
 
-_OPT = {"AdagradOptimizer": 0, "GradientDescentOptimizer": 1}
+# --optimizer names (FM.py:129-136, AFM.py:151-158, OurModel7.py:186-193) -> the
+# train kernels' optimizer codes (include/hhfm.h)
+_OPT = {"AdagradOptimizer": 0, "GradientDescentOptimizer": 1, "MomentumOptimizer": 2,
+        "AdamOptimizer": 3}
+_SGD = 1
 
 
 def _opt_code(model):
     try:
         return _OPT[model.optimizer_type]
     except KeyError:
-        raise NotImplementedError(f"optimizer {model.optimizer_type!r} (the kernels implement "
-                                  "AdagradOptimizer and GradientDescentOptimizer)")
+        raise NotImplementedError(f"optimizer {model.optimizer_type!r} (the reference accepts "
+                                  f"{', '.join(_OPT)})") from None
 
 
-def _state(model, names):
-    """Optimizer accumulators (TF initial_accumulator_value = 0.1) + the zeroed
-    gradient workspace, created on first use."""
+def _slots(opt, t):
+    """The optimizer's slot array for variable ``t``: Adagrad's accumulator
+    (TF initial_accumulator_value 0.1), Momentum's zeroed accumulator, Adam's
+    zeroed m then v (2 × numel); SGD keeps none (a 1-element placeholder)."""
+    if opt == 0:
+        return torch.full_like(t, 0.1)
+    if opt == 2:
+        return torch.zeros_like(t)
+    if opt == 3:
+        return torch.zeros(2 * t.numel(), dtype=t.dtype, device=t.device)
+    return torch.zeros(1, dtype=t.dtype, device=t.device)
+
+
+def _state(model, names, opt):
+    """Optimizer slots (``_slots``) + the zeroed gradient workspace (which also
+    carries Adam's β1^t, β2^t), created on first use."""
     st = getattr(model, "_train_state", None)
+    if st is not None and st.get("opt") != opt:
+        raise ValueError("the optimizer changed after the first partial_fit")
     if st is None:
         if model.table_dtype != torch.float32:
             raise NotImplementedError("training runs on fp32 tables")
-        st = {n: torch.full_like(model.weights[n], 0.1) for n in names}
+        st = {n: _slots(opt, model.weights[n]) for n in names}
+        st["opt"] = opt
         k = model.weights["feature_embeddings"].shape[1]
         nbytes = native().train_workspace(model.features_M, k)
         st["ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=model.device)
@@ -48,13 +68,22 @@ def _state(model, names):
     return st
 
 
+def _grow(old, nbytes, dev):
+    """A zero-filled train workspace of ``nbytes``; the persistent state at
+    its front (include/hhfm.h: gradients, Adam's β powers) carried over."""
+    ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    if old is not None:
+        ws[:old.numel()].copy_(old)
+    return ws
+
+
 def fm_partial_fit(model, data) -> float:
     """FM.partial_fit (FM.py:168-171): one optimizer step, returns the loss."""
     opt = _opt_code(model)
     if model.keep != 1:
         raise NotImplementedError("dropout keep < 1 is not implemented")
     W = model.weights
-    st = _state(model, ["feature_embeddings", "feature_bias", "bias"])
+    st = _state(model, ["feature_embeddings", "feature_bias", "bias"], opt)
     X = model._idx(data["X"])
     y = torch.as_tensor(np.asarray(data["Y"], np.float32).reshape(-1)).to(model.device)
     B, F = X.shape
@@ -74,7 +103,7 @@ def hhfm_partial_fit(model, data) -> float:
     F1 ctx columns, F2 time columns."""
     opt = _opt_code(model)
     W = model.weights
-    st = _state(model, ["feature_embeddings"])
+    st = _state(model, ["feature_embeddings"], opt)
     parts = [np.asarray(data["X"])]
     if model.context:
         parts.append(np.asarray(data["F1"]))
@@ -106,7 +135,7 @@ def dfm_partial_fit(model, data) -> float:
     if st is None:
         if model.table_dtype != torch.float32:
             raise NotImplementedError("training runs on fp32 tables")
-        st = {n: torch.full_like(W[n], 0.1) for n in names}
+        st = {n: _slots(0, W[n]) for n in names}
         st["loss"] = torch.zeros(1, dtype=torch.float32, device=model.device)
         st["ws"], st["ws_rows"] = None, 0
         model._train_state = st
@@ -118,7 +147,7 @@ def dfm_partial_fit(model, data) -> float:
     nat = native()
     if st["ws"] is None or st["ws_rows"] < B:
         nbytes = nat.dfm_train_workspace(B, F, k, M, dims)
-        st["ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=model.device)
+        st["ws"] = _grow(st["ws"], nbytes, model.device)
         st["ws_rows"] = B
     ptr = lambda n: W[n].data_ptr()  # noqa: E731
     nat.dfm_train_step(X.data_ptr(), y.data_ptr(), B, F, ptr("feature_embeddings"),
@@ -141,10 +170,13 @@ def afm_partial_fit(model, data) -> float:
     names = ["feature_embeddings", "feature_bias", "bias", "attention_W", "attention_b",
              "attention_p", "prediction"]
     st = getattr(model, "_train_state", None)
+    if st is not None and st.get("opt") != opt:
+        raise ValueError("the optimizer changed after the first partial_fit")
     if st is None:
         if model.table_dtype != torch.float32:
             raise NotImplementedError("training runs on fp32 tables")
-        st = {n: torch.full_like(W[n], 0.1) for n in names}
+        st = {n: _slots(opt, W[n]) for n in names}
+        st["opt"] = opt
         st["loss"] = torch.zeros(1, dtype=torch.float32, device=model.device)
         st["ws"], st["ws_rows"] = None, 0
         model._train_state = st
@@ -156,7 +188,7 @@ def afm_partial_fit(model, data) -> float:
     nat = native()
     if st["ws"] is None or st["ws_rows"] < B:
         nbytes = nat.afm_train_workspace(B, F, k, A, M)
-        st["ws"] = torch.zeros(nbytes, dtype=torch.uint8, device=model.device)
+        st["ws"] = _grow(st["ws"], nbytes, model.device)
         st["ws_rows"] = B
     lam = float(model.lamda_attention) if model.lamda_attention > 0 else 0.0
     ptr = lambda n: W[n].data_ptr()  # noqa: E731
@@ -164,7 +196,7 @@ def afm_partial_fit(model, data) -> float:
                        ptr("feature_bias"), ptr("bias"), M, k, A, ptr("attention_W"),
                        ptr("attention_b"), ptr("attention_p"), ptr("prediction"),
                        float(model.learning_rate), lam, opt,
-                       [st[n].data_ptr() for n in names] if opt == 0 else [],
+                       [st[n].data_ptr() for n in names] if opt != _SGD else [],
                        st["ws"].data_ptr(), st["ws"].numel(), st["loss"].data_ptr(),
                        ops._stream(model.device))
     return float(st["loss"].item())

@@ -346,11 +346,23 @@ int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, const vo
  * H6 — one training step (`partial_fit`, sess.run((loss, optimizer))).
  *   FM   (FM.py:123-136):        loss = Σ (y − out)²/2 + λ·Σ E²/2
  *   HHFM (OurModel7.py:172-193): loss = −Σ log σ(pos − max_j neg_j) + λ·Σ E²/2
- * optimizer 0 = TF AdagradOptimizer (accumulators initialised to 0.1 by the
- * caller; accum += g², var -= lr·g·rsqrt(accum)), 1 = GradientDescent.
+ * optimizer (TF-1.x semantics, FM.py:129-136; `acc` slots per variable):
+ *   0 = AdagradOptimizer  accum += g², var -= lr·g·rsqrt(accum); n floats
+ *       initialised to 0.1 (TF's initial_accumulator_value);
+ *   1 = GradientDescentOptimizer (no slots);
+ *   2 = MomentumOptimizer(momentum = 0.95)  accum = accum·0.95 + g,
+ *       var -= accum·lr; n floats initialised to 0;
+ *   3 = AdamOptimizer(β1 0.9, β2 0.999, ε 1e-8)  2n floats (m, then v)
+ *       initialised to 0; β1^t, β2^t live in the workspace (zero-filled
+ *       once = step 1).
+ * Variables whose TF gradient is an IndexedSlices (an embedding_lookup with
+ * no dense l2 term on the same variable: w of FM; the table of FM / HHFM at
+ * λ = 0, of DeepFM and of AFM; w of DeepFM and AFM) follow TF's sparse
+ * rules: Momentum updates only the rows the batch touched, Adam decays m
+ * and v of every row (AdamOptimizer._apply_sparse_shared).
  * E, w are fp32 and updated in place; *loss (device float) receives the loss
  * of the pre-update parameters.  The workspace (hhfm_train_workspace bytes)
- * must be zero-filled once; the step leaves it zeroed.  HHFM: X [B][ncols]
+ * must be zero-filled once; the step leaves it zeroed except Adam's β powers.  HHFM: X [B][ncols]
  * full rows [user, item, ctx..., time...], Neg [B][NG] negative item ids,
  * NG <= 16.
  * ---------------------------------------------------------------------- */
@@ -368,13 +380,16 @@ int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_t B, int32_
 
 /* DeepFM (DFM.py:139-155, 214-217; use_fm = use_deep = True, loss "mse"):
  *   loss = Σ (y − out)²/2 + λ·(‖Wp‖² + Σ_l ‖W_l‖²)/2
- * one step of TF Adagrad (optimizer 0) or gradient descent (1) on every
- * variable, in place.  W[l] is layer l row-major [d_{l-1}][d_l] (d_{-1} =
- * F·k), bias[l] [d_l], Wp the concat projection [F + k + d_{L-1}], bp a
- * device float.  acc (Adagrad): 2L+4 device accumulators in the order E, w,
- * W_0..W_{L-1}, b_0..b_{L-1}, Wp, bp, initialised to 0.1 by the caller.
+ * one step of the optimizer (codes as above) on every variable, in place.
+ * W[l] is layer l row-major [d_{l-1}][d_l] (d_{-1} = F·k), bias[l] [d_l], Wp
+ * the concat projection [F + k + d_{L-1}], bp a device float.  acc (every
+ * optimizer but 1): 2L+4 device slot arrays in the order E, w, W_0..W_{L-1},
+ * b_0..b_{L-1}, Wp, bp, sized and initialised as above.
  * The workspace (hhfm_dfm_train_workspace bytes for batches of at most B rows)
- * must be zero-filled once; the step keeps its gradient regions zeroed.
+ * must be zero-filled once; the step keeps its gradient regions zeroed.  Its
+ * persistent part (gradients, Adam's β powers) leads at offsets independent
+ * of B: a workspace grown for a larger batch keeps the state when the old
+ * bytes are copied into the front of the new zero-filled one.
  * Requires k % 4 == 0, L <= 4, F + k + d_{L-1} <= 1024. */
 int hhfm_dfm_train_workspace(int64_t B, int32_t F, int32_t k, int64_t features_M,
                              int32_t nlayers, const int32_t* layer_dims, size_t* ws_bytes);
@@ -387,13 +402,14 @@ int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F
 
 /* AFM (AFM.py:103-156, 205-207; attention = 1, keep = [1, 1]):
  *   loss = Σ (y − out)²/2 + λ·‖attention_W‖²/2
- * one step of TF Adagrad (optimizer 0) or gradient descent (1) on every
- * variable, in place: E [M][k], w [M], w0 (device float), W = attention_W
- * [k][A] row-major, b = attention_b [A], pvec = attention_p [A], P =
- * prediction [k].  acc (Adagrad): 7 device accumulators in the order E, w,
- * w0, W, b, pvec, P, initialised to 0.1 by the caller.  The workspace
+ * one step of the optimizer (codes as above) on every variable, in place:
+ * E [M][k], w [M], w0 (device float), W = attention_W [k][A] row-major,
+ * b = attention_b [A], pvec = attention_p [A], P = prediction [k].  acc
+ * (every optimizer but 1): 7 device slot arrays in the order E, w, w0, W, b,
+ * pvec, P, sized and initialised as above.  The workspace
  * (hhfm_afm_train_workspace bytes for batches of at most B rows) must be
- * zero-filled once; the step keeps its gradient regions zeroed.
+ * zero-filled once; the step keeps its gradient regions zeroed; grown as for
+ * DeepFM (old bytes copied into the front of the new one).
  * Requires 2 <= F <= 16, k and A multiples of 4 and <= 256.  Replaces
  * sess.run((loss, optimizer)) of AFM.partial_fit (AFM.py:205-207). */
 int hhfm_afm_train_workspace(int64_t B, int32_t F, int32_t k, int32_t A,

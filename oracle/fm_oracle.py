@@ -285,7 +285,65 @@ def tf_adagrad(var, grad, acc, lr):
     return (var - F32(lr) * grad / np.sqrt(acc)).astype(F32), acc
 
 
-def fm_train_step(X, y, E, w, w0, accE, accw, accw0, lr, lam, optimizer="adagrad"):
+MOMENTUM, BETA1, BETA2, ADAM_EPS = F32(0.95), F32(0.9), F32(0.999), F32(1e-8)
+
+
+def adam_powers(step):
+    """TF AdamOptimizer's beta1_power / beta2_power at ``step`` (1-based):
+    created at β1, β2 and multiplied by β in float32 after every step (_finish)."""
+    b1p, b2p = BETA1, BETA2
+    for _ in range(step - 1):
+        b1p, b2p = F32(b1p * BETA1), F32(b2p * BETA2)
+    return b1p, b2p
+
+
+def tf_apply(optimizer, var, grad, slot, lr, step=1, rows=None):
+    """One TF-1.x optimizer update of ``var`` (FM.py:129-136, AFM.py:151-158,
+    OurModel7.py:186-193).  ``rows``: None for a dense gradient, else the ids of
+    the IndexedSlices an embedding_lookup produced (duplicates allowed; TF sums
+    them first).  slot: Adagrad's accumulator, Momentum's accumulator, Adam's
+    m and v stacked as a flat [2·n] array, None for SGD.  Returns (var, slot).
+    * Adagrad (ApplyAdagrad; the sparse kernel is the same on touched rows and
+      a no-op on the others): accum += g²; var -= lr·g/√accum.
+    * Momentum(0.95) dense: accum = accum·0.95 + g; var -= lr·accum; sparse:
+      the same on the touched rows only.
+    * Adam(0.9, 0.999, 1e-8), α = lr·√(1−β2^t)/(1−β1^t): dense ApplyAdam
+      m += (g−m)(1−β1), v += (g²−v)(1−β2); sparse (_apply_sparse_shared)
+      m = m·β1 + g(1−β1), v = v·β2 + g²(1−β2) on every row; var -= α·m/(√v+ε)."""
+    var = np.asarray(var, F32)
+    g = np.asarray(grad, F32).reshape(var.shape)
+    lr = F32(lr)
+    if optimizer == "adagrad":
+        return tf_adagrad(var, g, np.asarray(slot, F32).reshape(var.shape), lr)
+    if optimizer == "sgd":
+        return (var - lr * g).astype(F32), slot
+    if optimizer == "momentum":
+        acc = np.asarray(slot, F32).reshape(var.shape).copy()
+        if rows is None:
+            acc = (acc * MOMENTUM + g).astype(F32)
+            return (var - acc * lr).astype(F32), acc
+        var = var.copy()
+        t = np.unique(np.asarray(rows, np.int64).reshape(-1))
+        acc[t] = acc[t] * MOMENTUM + g[t]
+        var[t] = var[t] - acc[t] * lr
+        return var, acc
+    if optimizer == "adam":
+        mv = np.asarray(slot, F32).reshape(2, *var.shape)
+        m, v = mv[0], mv[1]
+        b1p, b2p = adam_powers(step)
+        alpha = F32(lr * np.sqrt(F32(1) - b2p, dtype=F32) / (F32(1) - b1p))
+        if rows is None:
+            m = (m + (g - m) * (F32(1) - BETA1)).astype(F32)
+            v = (v + (g * g - v) * (F32(1) - BETA2)).astype(F32)
+        else:
+            m = (m * BETA1 + g * (F32(1) - BETA1)).astype(F32)
+            v = (v * BETA2 + (g * g) * (F32(1) - BETA2)).astype(F32)
+        var = (var - (m * alpha) / (np.sqrt(v) + ADAM_EPS)).astype(F32)
+        return var, np.stack([m, v]).reshape(-1)
+    raise ValueError(f"optimizer {optimizer!r}")
+
+
+def fm_train_step(X, y, E, w, w0, accE, accw, accw0, lr, lam, optimizer="adagrad", step=1):
     """FM partial_fit (FM.py:123-136, 168-171): loss = Σ(y−out)²/2 + λ·ΣE²/2.
     Returns (loss, E, w, w0, accE, accw, accw0) after one update."""
     X = np.asarray(X, np.int64)
@@ -306,17 +364,15 @@ def fm_train_step(X, y, E, w, w0, accE, accw, accw0, lr, lam, optimizer="adagrad
     for f in range(X.shape[1]):
         np.add.at(dw, X[:, f], g)
     dw0 = F32(g.sum())
-    if optimizer == "adagrad":
-        E, accE = tf_adagrad(E, dE, accE, lr)
-        w, accw = tf_adagrad(w, dw, accw, lr)
-        w0n, accw0 = tf_adagrad(np.float32(w0), dw0, np.float32(accw0), lr)
-    else:
-        E, w, w0n = E - F32(lr) * dE, w - F32(lr) * dw, F32(w0) - F32(lr) * dw0
+    # E is an IndexedSlices unless the l2 term adds a dense gradient; w always is
+    E, accE = tf_apply(optimizer, E, dE, accE, lr, step, X if lam == 0 else None)
+    w, accw = tf_apply(optimizer, w, dw, accw, lr, step, X)
+    w0n, accw0 = tf_apply(optimizer, np.float32(w0), dw0, accw0, lr, step)
     return loss, E, w, F32(w0n), accE, accw, accw0
 
 
 def hhfm_train_step(X, Neg, E, accE, lr, lam, feature_dimension, time_dimension,
-                    context=True, time=False, optimizer="adagrad"):
+                    context=True, time=False, optimizer="adagrad", step=1):
     """OUR partial_fit (OurModel7.py:171-193): loss = −Σ log σ(pos − max_j neg_j)
     + λ·ΣE²/2; reduce_max's gradient is split equally between tied maxima."""
     X = np.asarray(X, np.int64)
@@ -345,14 +401,13 @@ def hhfm_train_step(X, Neg, E, accE, lr, lam, feature_dimension, time_dimension,
             for c in range(cols.shape[1]):
                 np.add.at(dE, np.asarray(cols)[:, c].astype(np.int64), dh)
     dE += F32(lam) * E
-    if optimizer == "adagrad":
-        E, accE = tf_adagrad(E, dE, accE, lr)
-    else:
-        E = E - F32(lr) * dE
+    rows = np.concatenate([X.reshape(-1), Neg.reshape(-1)]) if lam == 0 else None
+    E, accE = tf_apply(optimizer, E, dE, accE, lr, step, rows)
     return loss, E, accE
 
 
-def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="adagrad"):
+def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="adagrad",
+                   step=1):
     """DeepFM partial_fit (DFM.py:139-155, 214-217), use_fm = use_deep = True,
     loss_type "mse": loss = l2_loss(y − out) + λ·(‖Wp‖² + Σ_l ‖W_l‖²)/2
     (l2_regularizer on concat_projection and every layer_i; not on the
@@ -400,14 +455,12 @@ def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="
         np.add.at(dw, X[:, f], dcat[:, f])
     acc = {key: np.asarray(v, F32).copy() for key, v in acc.items()}
 
-    def upd(var, grad, key):
-        if optimizer == "adagrad":
-            var, acc[key] = tf_adagrad(var, grad, acc[key], lr)
-            return var
-        return (var - F32(lr) * grad).astype(F32)
+    def upd(var, grad, key, rows=None):
+        var, acc[key] = tf_apply(optimizer, var, grad, acc.get(key), lr, step, rows)
+        return var
 
-    E = upd(E, dE, "E")
-    w = upd(w, dw, "w")
+    E = upd(E, dE, "E", X)
+    w = upd(w, dw, "w", X)
     layers = [upd(W, dW, f"W{i}") for i, (W, dW) in enumerate(zip(layers, dWs))]
     biases = [upd(b, db, f"b{i}") for i, (b, db) in enumerate(zip(biases, dbs))]
     Wp = upd(Wp, dWp, "Wp")
@@ -415,7 +468,7 @@ def dfm_train_step(X, y, E, w, layers, biases, Wp, bp, acc, lr, lam, optimizer="
     return loss, E, w, layers, biases, Wp, F32(bp), acc
 
 
-def afm_train_step(X, y, E, w, w0, W, b, pvec, P, acc, lr, lam, optimizer="adagrad"):
+def afm_train_step(X, y, E, w, w0, W, b, pvec, P, acc, lr, lam, optimizer="adagrad", step=1):
     """AFM partial_fit (AFM.py:144-156, 205-207), attention=1, keep=[1,1]:
     loss = l2_loss(y − out) + l2_regularizer(λ)(attention_W) = Σ(y−out)²/2
     + λ·ΣW²/2, one TF step on every variable (feature_embeddings,
@@ -470,11 +523,9 @@ def afm_train_step(X, y, E, w, w0, W, b, pvec, P, acc, lr, lam, optimizer="adagr
         np.add.at(dw, X[:, f], g)
     acc = {key: np.asarray(v, F32).copy() for key, v in acc.items()}
 
-    def upd(var, grad, key):
-        if optimizer == "adagrad":
-            var, acc[key] = tf_adagrad(var, grad, acc[key].reshape(np.shape(var)), lr)
-            return var
-        return (var - F32(lr) * grad).astype(F32)
+    def upd(var, grad, key, rows=None):
+        var, acc[key] = tf_apply(optimizer, var, grad, acc.get(key), lr, step, rows)
+        return var
 
-    return (loss, upd(E, dE, "E"), upd(w, dw, "w"), F32(upd(np.float32(w0), dw0, "w0")),
+    return (loss, upd(E, dE, "E", X), upd(w, dw, "w", X), F32(upd(np.float32(w0), dw0, "w0")),
             upd(W, dW, "W"), upd(b, db, "b"), upd(pvec, dpvec, "p"), upd(P, dP, "P"), acc)

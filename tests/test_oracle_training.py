@@ -166,3 +166,52 @@ def test_afm_gradient_matches_finite_differences():
         grad = (args[which].astype(np.float32)[i] - new[which][i]) / lr
         ref = fd(which, i)
         assert np.isclose(grad, ref, rtol=3e-3, atol=3e-4), (which, i, grad, ref)
+
+
+def test_tf_momentum_dense_and_sparse():
+    """MomentumOptimizer(0.95) (FM.py:135-136): ApplyMomentum on a dense
+    gradient, SparseApplyMomentum (touched rows only) on an IndexedSlices."""
+    v = np.float32([[1.0, 2.0], [3.0, 4.0], [5.0, 6.0]])
+    g = np.float32([[0.5, -1.0], [0.0, 0.0], [2.0, 0.25]])
+    acc = np.float32([[0.1, 0.2], [0.3, 0.4], [0.5, 0.6]])
+    v1, a1 = orc.tf_apply("momentum", v, g, acc, 0.1)
+    assert np.array_equal(a1, (acc * np.float32(0.95) + g).astype(np.float32))
+    assert np.allclose(v1, v - 0.1 * a1)
+    # ids [2, 0, 2]: row 1 untouched keeps var and accumulator; a touched row
+    # with a zero gradient still decays
+    v2, a2 = orc.tf_apply("momentum", v, g, acc, 0.1, rows=np.array([2, 0, 2]))
+    assert np.array_equal(v2[1], v[1]) and np.array_equal(a2[1], acc[1])
+    assert np.array_equal(a2[[0, 2]], a1[[0, 2]]) and np.allclose(v2[[0, 2]], v1[[0, 2]])
+    g0 = np.zeros_like(g)
+    v3, a3 = orc.tf_apply("momentum", v, g0, acc, 0.1, rows=np.array([1]))
+    assert np.allclose(a3[1], acc[1] * 0.95) and np.allclose(v3[1], v[1] - 0.1 * a3[1])
+    assert np.array_equal(v3[0], v[0])
+
+
+def test_tf_adam_dense_and_sparse():
+    """AdamOptimizer(0.9, 0.999, 1e-8) (FM.py:129-130): β powers start at β
+    and advance after each step; the first step moves every coordinate with a
+    gradient by ≈ lr·sign(g); sparse Adam decays m, v and moves untouched rows."""
+    assert orc.adam_powers(1) == (np.float32(0.9), np.float32(0.999))
+    b1p, b2p = orc.adam_powers(3)
+    assert b1p == np.float32(np.float32(np.float32(0.9) * np.float32(0.9)) * np.float32(0.9))
+    assert abs(b2p - 0.999 ** 3) < 1e-6
+    v = np.float32([1.0, -2.0, 0.5, 3.0])
+    g = np.float32([0.3, -0.02, 0.0, 5.0])
+    slot = np.zeros(8, np.float32)
+    v1, s1 = orc.tf_apply("adam", v, g, slot, 0.01, step=1)
+    assert np.allclose(v - v1, 0.01 * np.sign(g), rtol=1e-4, atol=1e-7)
+    assert np.allclose(s1[:4], 0.1 * g) and np.allclose(s1[4:], 0.001 * g * g, rtol=1e-4)  # f32 1−β2
+    # float64 restatement of step 2 (dense)
+    v2, s2 = orc.tf_apply("adam", v1, g, s1, 0.01, step=2)
+    m = 0.9 * s1[:4].astype(np.float64) + 0.1 * g
+    vv = 0.999 * s1[4:].astype(np.float64) + 0.001 * g.astype(np.float64) ** 2
+    alpha = 0.01 * np.sqrt(1 - 0.999 ** 2) / (1 - 0.9 ** 2)
+    assert np.allclose(v2, v1 - alpha * m / (np.sqrt(vv) + 1e-8), rtol=1e-6, atol=1e-7)
+    # sparse: the id list touches 0 and 3 only, yet every row with m != 0 moves
+    E = np.float32([[1.0], [2.0], [3.0], [4.0]])
+    gs = np.float32([[0.5], [0.0], [0.0], [-0.5]])
+    E1, t1 = orc.tf_apply("adam", E, gs, np.zeros(8, np.float32), 0.1, 1, rows=np.array([0, 3]))
+    assert E1[1, 0] == E[1, 0] and E1[2, 0] == E[2, 0]     # m = 0 there: no move
+    E2, t2 = orc.tf_apply("adam", E1, np.zeros_like(gs), t1, 0.1, 2, rows=np.array([1]))
+    assert np.allclose(t2[:4], 0.9 * t1[:4]) and E2[0, 0] < E1[0, 0] and E2[3, 0] > E1[3, 0]
