@@ -52,7 +52,11 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU-baseline time budget (0 disables)")
     p.add_argument("--cpu-rows", type=int, default=1 << 21)
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_fm_rows.json"),
+                   help="calibrated PMC bytes/row, used only when the in-run PMC passes "
+                        "cannot run (no rocprofv3, --no-pmc, or a failed pass)")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the in-run rocprofv3 --pmc passes for roofline.traffic")
     p.add_argument("--legs", default="hr,catalog,catalog_bf16,c3,c5",
                    help="extra legs: hr (HR@10 identity after GPU training on Frappe-shape "
                         "data), catalog / catalog_bf16 (C4 item-sharded top-K over an fp32 / "
@@ -665,6 +669,70 @@ def _c5_parity(m, X, out, mlp):
             "oracle_s": time.perf_counter() - t0}
 
 
+def _pmc_column(path):
+    """Per-dispatch Counter_Value of fm_rows_fast from a rocprofv3 --pmc csv."""
+    import csv
+    with open(path) as f:
+        return [float(r["Counter_Value"]) for r in csv.DictReader(f)
+                if "fm_rows_fast" in r["Kernel_Name"]]
+
+
+def pmc_bytes_per_row(fetch, write, rows, k):
+    """HBM bytes per K1 row from the six fm_rows_fast dispatches of
+    scripts/pmc_fm_rows.py (calib x2, bench x2, bench-without-w x2):
+    FETCH_SIZE is scaled by the calibration launch, whose user/item rows are
+    streamed once (known bytes; MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE
+    tallies 128-B requests at 64 B); WRITE_SIZE is exact for the output's
+    streaming stores.  fetch / write: the two passes' KB values."""
+    if len(fetch) != 6 or len(write) != 6:
+        raise ValueError(f"expected 6 fm_rows_fast dispatches, got {len(fetch)} / {len(write)}")
+    known = rows * (2 * k * 4 + 5 * 4 + 2 * 4)
+    calib = 1024.0 * (fetch[0] + fetch[1]) / 2
+    factor = known / calib
+    rd = 1024.0 * (fetch[2] + fetch[3]) / 2 * factor / rows
+    wr = 1024.0 * (write[2] + write[3]) / 2 / rows
+    rd_now = 1024.0 * (fetch[4] + fetch[5]) / 2 * factor / rows
+    wr_now = 1024.0 * (write[4] + write[5]) / 2 / rows
+    return {"hbm_read_bytes_per_row": rd, "hbm_write_bytes_per_row": wr,
+            "hbm_bytes_per_row": rd + wr, "no_w_hbm_bytes_per_row": rd_now + wr_now,
+            "w_gather_bytes_per_row": rd - rd_now,
+            "calibration": {"known_bytes_per_launch": known, "fetch_size_bytes": calib,
+                            "factor": factor},
+            "fetch_size_kb": fetch, "write_size_kb": write, "pmc_rows": rows}
+
+
+def pmc_traffic(rows, k, timeout_s=150):
+    """K1's HBM bytes per row read from PMC counters in this run: two
+    rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: they cannot share a
+    pass) over scripts/pmc_fm_rows.py at this bench's row count and table,
+    each a child process under its own kill timeout.  Returns (dict, None)
+    or (None, reason)."""
+    import shutil
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None, "rocprofv3 not on PATH"
+    tmp = tempfile.mkdtemp(prefix="hhfm_pmc_")
+    env = dict(os.environ, PMC_ROWS=str(rows), PMC_K=str(k))
+    vals = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr.lower())
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), exe, "--pmc", ctr, "-d", d,
+                   "-o", "pmc", "--output-format", "csv", "--", sys.executable,
+                   os.path.join(ROOT, "scripts", "pmc_fm_rows.py")]
+            r = subprocess.run(cmd, env=env, cwd=tmp, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                return None, f"{ctr} pass exited {r.returncode}: {r.stderr[-300:]}"
+            vals[ctr] = _pmc_column(os.path.join(d, "pmc_counter_collection.csv"))
+        return pmc_bytes_per_row(vals["FETCH_SIZE"], vals["WRITE_SIZE"], rows, k), None
+    except (OSError, ValueError, KeyError) as e:
+        return None, f"{type(e).__name__}: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
 def stream_read_peak(buf, reps=5):
     """The box's measured HBM read ceiling: hhfm_probe_stream_read over
     `buf` (grid-stride, contiguous-chunk and non-temporal chunk variants),
@@ -777,16 +845,27 @@ def main():
     bpr_lines = 2 * args.k * 4 + 2 * 128 + 5 * 4 + 4
     peak_meas, peak_variants = stream_read_peak(E)
     gather_peak, gather_ms = gather_rows_peak(idx, E)
-    traffic = None
-    if os.path.exists(args.traffic_json):
+    traffic, pmc, why = None, None, "--no-pmc"
+    if rank == 0 and world == 1 and not args.no_pmc:
+        pmc, why = pmc_traffic(args.rows, args.k)
+    if pmc is not None:
+        # PMC bytes per row of this run (corrected FETCH_SIZE + WRITE_SIZE) x rows per launch
+        traffic = pmc["hbm_bytes_per_row"] * args.rows
+        traffic_source = ("measured in this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
+                          "passes (child processes) over scripts/pmc_fm_rows.py at "
+                          f"{args.rows} rows, FETCH_SIZE calibrated on a known-byte launch")
+    elif os.path.exists(args.traffic_json):
+        traffic_source = (f"calibrated, not measured in this run ({why}): PMC bytes/row from "
+                          f"{os.path.relpath(args.traffic_json, ROOT)} x rows")
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("k") == args.k and tj.get("fields") == 5:
-                # PMC bytes per row (calibrated FETCH_SIZE + WRITE_SIZE) x rows per launch
                 traffic = tj["hbm_bytes_per_row"] * args.rows
         except (OSError, ValueError):
             traffic = None
+    else:
+        traffic_source = f"none ({why})"
 
     result = {
         "metric": METRIC, "value": value, "unit": "triples/s", "n_gpus": world,
@@ -823,9 +902,8 @@ def main():
                      "line_rate_GBps": bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9,
                      "line_frac_vs_measured": (bpr_lines * args.rows / (kern_ms * 1e-3) / 1e9
                                                / peak_meas) if peak_meas else None,
-                     "traffic_source": "calibrated, not measured in this run: PMC bytes/row "
-                                       "from profiles/traffic_fm_rows.json (separate "
-                                       "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes) x rows"},
+                     "traffic_source": traffic_source,
+                     "traffic_pmc": pmc},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(idx, E, w, w0, out, args)

@@ -12,6 +12,7 @@ Two launches of the headline kernel on the bench table (16.8 M x 64 fp32):
      the cost of the two 4-byte w gathers per row).
 Run under: rocprofv3 --pmc FETCH_SIZE ... -- python scripts/pmc_fm_rows.py
            rocprofv3 --pmc WRITE_SIZE ... -- python scripts/pmc_fm_rows.py
+(bench.py's pmc_traffic runs both passes at the bench's row count)
 """
 import os
 import sys
@@ -24,8 +25,9 @@ import bench  # noqa: E402
 from hhfm_amd import ops  # noqa: E402
 
 rows = int(os.environ.get("PMC_ROWS", 1 << 23))
+k = int(os.environ.get("PMC_K", 64))
 dev = torch.device("cuda", 0)
-idx, E, w, M = bench.make_batch(rows, 8 << 20, 8 << 20, 64, 1, dev)
+idx, E, w, M = bench.make_batch(rows, 8 << 20, 8 << 20, k, 1, dev)
 out = torch.empty(rows, dtype=torch.float32, device=dev)
 seq = idx.clone()
 r = torch.arange(rows, device=dev, dtype=torch.int32)

@@ -48,19 +48,21 @@ def _slot(o, v):
 
 def _check_var(got, ref, before, o, grad):
     """_close_update, except under Adam: its early steps move an element by
-    ≈ ±α whatever |g| is, so an element whose gradient sits at the float
-    atomics' summation-order noise (|g| < 1e-3 · max|g|) may take the other
-    sign; those are held only to that bound (≤ 2 × the largest step)."""
+    ≈ ±α whatever |g| is, so an element whose gradient sits near the float
+    atomics' summation-order noise (|g| < 1e-4 of its table row's largest
+    |g|, of the whole variable's for a vector) may take the other sign; those
+    are held only to that bound (≤ 2 × the largest step)."""
     got, ref, before = (np.asarray(x, np.float32) for x in (got, ref, before))
     if o != "adam":
         _close_update(got, ref, before)
         return
     g = np.abs(np.asarray(grad, np.float32).reshape(ref.shape))
-    well = g >= 1e-3 * g.max() if g.size else g
+    scale = g.max(axis=-1, keepdims=True) if g.ndim == 2 else g.max(initial=0.0)
+    well = g >= 1e-4 * scale
     step = np.abs(ref - before).max()
     assert np.allclose(got[well], ref[well], rtol=1e-5, atol=1e-4 * step + 1e-9)
     assert np.all(np.abs(got - ref) <= 2.01 * step + 1e-9)
-    assert (~well & (g > 0)).mean() < 0.05
+    assert (well & (g > 0)).sum() >= 0.9 * (g > 0).sum()
 
 
 def _check_slot(got, ref, o):
