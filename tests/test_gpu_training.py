@@ -261,6 +261,11 @@ def test_afm_partial_fit_matches_oracle(k, A, ctx, B, opt):
     W["feature_bias"] = rng.normal(0, 0.01, (M, 1)).astype(np.float32)
     W["prediction"] = rng.normal(1, 0.2, (k, 1)).astype(np.float32)
     m.set_weights(feature_bias=W["feature_bias"], prediction=W["prediction"])
+    if opt in ("MomentumOptimizer", "AdamOptimizer"):
+        # at the 0.01 init every pair's pre-activation has the sign of its
+        # bias, so d attention_b = p · Σ_pairs dlogit = 0 exactly and both
+        # sides hold only summation noise in that slot: spread the pairs
+        m.set_weights(feature_embeddings=rng.normal(0, 0.3, (M, k)).astype(np.float32))
     names = ["feature_embeddings", "feature_bias", "bias", "attention_W", "attention_b",
              "attention_p", "prediction"]
     keys = ["E", "w", "w0", "W", "b", "p", "P"]
