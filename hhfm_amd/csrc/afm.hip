@@ -368,12 +368,10 @@ __global__ __launch_bounds__(256, NT <= 2 ? 3 : NT == 3 ? 2 : 1) void afm_rows_f
 // the 32 rows at once — no per-row serial epilogue, all 32 columns live
 // (afm_rows_fused packs floor(32/np) rows of np pairs: 30 of 32 at F = 5,
 // and its softmax runs one lane per row).  F <= 8.
-#ifndef HHFM_AFM_PAIR_PF
-#define HHFM_AFM_PAIR_PF 0   // gathers in flight: 0 = a whole pair ahead, 1 = one 16-k step
-#endif
-#ifndef HHFM_AFM_PAIR_OCC
-#define HHFM_AFM_PAIR_OCC 2  // __launch_bounds__ minimum workgroups per CU (A/B)
-#endif
+// One 16-k step of gathers in flight at three workgroups per CU: against a
+// whole pair's gathers in flight at two, 0.556-0.572 vs 0.638-0.654 ms (bf16
+// table) and 0.619-0.634 vs 0.638-0.642 (fp32) per 1 M Frappe rows
+// (profiles/r04_afm_pairs_pf_occ_ab.txt; four per CU: 0.68 / 0.70 ms).
 
 // LDS: the three Wᵀ piece images, P, b, p, then per wave the rows' ids
 // [F][32] and the pair slots [np][32] (sized per call: F = 5 needs 40 KB at
@@ -385,7 +383,7 @@ static size_t afm_rows_pairs_lds(int NA, int K, int F) {
 }
 
 template <bool TBF, int NT, int KS>
-__global__ __launch_bounds__(256, HHFM_AFM_PAIR_OCC) void afm_rows_pairs(
+__global__ __launch_bounds__(256, 3) void afm_rows_pairs(
     const int32_t* __restrict__ idx, int64_t B, int F, const void* __restrict__ E, int64_t M,
     const float* __restrict__ w, float w0, const float* __restrict__ Wt,
     const float* __restrict__ att_b, const float* __restrict__ att_p, int A,
@@ -461,21 +459,10 @@ __global__ __launch_bounds__(256, HHFM_AFM_PAIR_OCC) void afm_rows_pairs(
     };
     int pi = 0, pj = 1;
     int32_t ia = il[j], ib = il[32 + j];
-#if HHFM_AFM_PAIR_PF == 1
-    // one 16-k step of gathers in flight (fewer registers)
+    // one 16-k step of gathers in flight
     float xa[1][8], ya[1][8];
     gather(ia, 0, xa[0]);
     gather(ib, 0, ya[0]);
-#else
-    // a whole pair's gathers in flight: step t of pair p+1 issued after step
-    // t of pair p consumed its registers
-    float xa[KS][8], ya[KS][8];
-#pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      gather(ia, t, xa[t]);
-      gather(ib, t, ya[t]);
-    }
-#endif
     for (int p = 0; p < np; ++p) {
       // the next pair's rows (read now, gathered during this pair's MFMAs)
       int ni = pi, nj = pj + 1;
@@ -506,7 +493,6 @@ __global__ __launch_bounds__(256, HHFM_AFM_PAIR_OCC) void afm_rows_pairs(
       for (int t = 0; t < KS; ++t) {
         float pe[8];
         const int c0 = 16 * t + 4 * h;
-#if HHFM_AFM_PAIR_PF == 1
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           pe[e] = xa[0][e] * ya[0][e];
@@ -519,17 +505,6 @@ __global__ __launch_bounds__(256, HHFM_AFM_PAIR_OCC) void afm_rows_pairs(
           gather(na, 0, xa[0]);
           gather(nb, 0, ya[0]);
         }
-#else
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          pe[e] = xa[t][e] * ya[t][e];
-          sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
-        }
-        if (more) {                                   // step t of the next pair
-          gather(na, t, xa[t]);
-          gather(nb, t, ya[t]);
-        }
-#endif
         bf16x8 b0, b1, b2;
         split3x8(pe, b0, b1, b2);
 #pragma unroll

@@ -56,10 +56,6 @@ constexpr int kWideRows = 192;
 #ifndef HHFM_WPI
 #define HHFM_WPI 1
 #endif
-// A fragments read from the weight ring 1 (default) or 2 k32 steps ahead
-#ifndef HHFM_WPF
-#define HHFM_WPF 1
-#endif
 
 template <int B_, int E_, class Fn>
 HHFM_DEV void static_for(Fn&& fn) {
@@ -479,30 +475,23 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) accN[rt][j] = bnext[j];
       }
+      // A fragments read from the weight ring two k32 steps ahead (one step
+      // ahead: 12.87-12.93 vs 12.80-12.83 ms at C5, profiles/r04_k3w_wpf_ab.txt)
       uint4 fa0 = wsl[0], fa1 = wsl[64];
-#if HHFM_WPF == 2
       uint4 fb0 = fa0, fb1 = fa1;
       if (S > 1) {
         fb0 = wsl[128];
         fb1 = wsl[192];
       }
-#endif
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const bf16x8 a0 = __builtin_bit_cast(bf16x8, fa0), a1 = __builtin_bit_cast(bf16x8, fa1);
-#if HHFM_WPF == 2   // A fragments two k32 steps ahead
         fa0 = fb0;
         fa1 = fb1;
         if (s + 2 < S) {
           fb0 = wsl[128 * (s + 2)];
           fb1 = wsl[128 * (s + 2) + 64];
         }
-#else
-        if (s + 1 < S) {
-          fa0 = wsl[128 * (s + 1)];
-          fa1 = wsl[128 * (s + 1) + 64];
-        }
-#endif
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt) {
           uint4 bx;
