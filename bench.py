@@ -712,6 +712,9 @@ def pmc_traffic(rows, k, timeout_s=150):
     exe = shutil.which("rocprofv3")
     if exe is None:
         return None, "rocprofv3 not on PATH"
+    if "rocprof" in os.environ.get("LD_PRELOAD", "") or any(
+            k.startswith("ROCPROF") for k in os.environ):
+        return None, "the bench itself runs under rocprofv3"
     tmp = tempfile.mkdtemp(prefix="hhfm_pmc_")
     env = dict(os.environ, PMC_ROWS=str(rows), PMC_K=str(k))
     vals = {}
