@@ -42,6 +42,23 @@ HHFM_DEV void split3x8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) 
   p2 = __builtin_bit_cast(bf16x8, w2);
 }
 
+// x with at most 16 significant bits (a product of two bf16 values, exact in
+// fp32) -> two bf16 pieces, x == p0 + p1 exactly: x − RNE(x) is a multiple of
+// x's last bit no larger than 2^7 of them, so 8 bits hold it (split3x8's
+// third piece of such x is +0).
+HHFM_DEV void split2x8(const float (&x)[8], bf16x8& p0, bf16x8& p1) {
+  u32x4_t w0, w1;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const float a = x[2 * v], b = x[2 * v + 1];
+    const uint32_t u0 = bf16x2_rne(a, b);
+    w0[v] = u0;
+    w1[v] = bf16x2_rne(a - __uint_as_float(u0 << 16), b - __uint_as_float(u0 & 0xffff0000u));
+  }
+  p0 = __builtin_bit_cast(bf16x8, w0);
+  p1 = __builtin_bit_cast(bf16x8, w1);
+}
+
 constexpr int GBM = 128, GBN = 128;
 
 // Column order of the projected layer 0 for the bf16 fused DeepFM kernel
