@@ -478,9 +478,14 @@ __global__ __launch_bounds__(256, 3) void afm_rows_pairs(
     };
     int pi = 0, pj = 1;
     int32_t ia = il[j], ib = il[32 + j];
-    // one 16-k step of gathers in flight
-    float xa[1][8], ya[1][8];
-    gather(ia, 0, xa[0]);
+    // pairs run i-major, (i, i+1) .. (i, F−1): row i's k slice is gathered
+    // once per run (all KS steps held), row j's one 16-k step ahead
+    // (row i held across its run: 0.627 -> 0.548 ms per 1 M rows, fp32 table;
+    // row j two steps ahead, or two workgroups per CU: slower,
+    // profiles/r04_afm_xrun_ab.txt, r04_afm_ypf_occ_ab.txt)
+    float xh[KS][8], ya[1][8];
+#pragma unroll
+    for (int t = 0; t < KS; ++t) gather(ia, t, xh[t]);
     gather(ib, 0, ya[0]);
     for (int p = 0; p < np; ++p) {
       // the next pair's rows (read now, gathered during this pair's MFMAs)
@@ -514,16 +519,14 @@ __global__ __launch_bounds__(256, 3) void afm_rows_pairs(
         const int c0 = 16 * t + 4 * h;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          pe[e] = xa[0][e] * ya[0][e];
+          pe[e] = xh[t][e] * ya[0][e];
           sP = fmaf(pe[e], Pl[c0 + (e < 4 ? e : e + 4)], sP);
         }
-        if (t + 1 < KS) {                             // the next step
-          gather(ia, t + 1, xa[0]);
+        if (t + 1 < KS)                               // the next step of row j
           gather(ib, t + 1, ya[0]);
-        } else if (more) {                            // the next pair's first step
-          gather(na, 0, xa[0]);
+        else if (more)                                // the next pair's first step
           gather(nb, 0, ya[0]);
-        }
+        if (more && ni != pi) gather(na, t, xh[t]);   // a new run: step t of row i
         // bf16 table: the pair product has <= 16 significant bits, two pieces
         // (the third is +0, its MFMA skipped: the same sums)
         bf16x8 b0, b1, b2;
