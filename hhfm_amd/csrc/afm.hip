@@ -1000,8 +1000,7 @@ __global__ __launch_bounds__(512) void afm_cat_w(
     const float* __restrict__ Wt, const float* __restrict__ att_b,
     const float* __restrict__ att_p, int A, const float* __restrict__ P,
     const float* __restrict__ ufdot, const float* __restrict__ suma, int64_t item_row_begin,
-    int32_t N, int tiles_per_block, int nchunk, const float* __restrict__ w,
-    float* __restrict__ scores) {
+    int32_t N, const float* __restrict__ w, float* __restrict__ scores) {
   constexpr int NA = NT * 32, K = 16 * KS, U2 = K / 8;   // 16-B chunks per unit row
   // swizzle mask: the largest power of two (<= 16) that DIVIDES U2, so the
   // XOR stays inside the unit's row (U2 = 6 at k = 48: mask 1, not 3)
@@ -1016,18 +1015,32 @@ __global__ __launch_bounds__(512) void afm_cat_w(
   float* apl = bl + NA;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const int j = l & 31, h = l >> 5;
-  const int64_t b = blockIdx.x / nchunk;
-  const int chunk = (int)(blockIdx.x - b * nchunk);
+  for (int x = tid; x < NA; x += 512) {
+    bl[x] = x < A ? att_b[x] : 0.f;
+    apl[x] = x < A ? att_p[x] : 0.f;
+  }
+  // persistent (one block per CU, the images take 98 KB at k = A = 64): this
+  // block's equal share [g0, g1) of the query-major (query b, item tile t)
+  // order; the W'' images are rebuilt once per query the share touches
+  // (one (query, chunk) per block rebuilt them for every 4 tiles per wave and
+  // left a partial last round of blocks: 300-query call 0.29 -> 0.26 ms,
+  // profiles/r04_afm_cat_persist_ab.txt)
+  const int ntile = (N + 31) / 32;
+  const int64_t T = nq * ntile;
+  int64_t g0 = T * blockIdx.x / gridDim.x;
+  const int64_t g1 = T * (blockIdx.x + 1) / gridDim.x;
+  while (g0 < g1) {
+  const int64_t b = g0 / ntile;
+  const int t0 = (int)(g0 - b * ntile);
+  const int t1 = (int)min<int64_t>(ntile, t0 + (g1 - g0));
+  g0 += t1 - t0;
+  __syncthreads();                   // the previous query's images are no longer read
   // uf of the query: [E[q0], E[q2], ..., E[q_{F-1}]]  (AFM.py:210-212)
   for (int x = tid; x < uF * K; x += 512) {
     const int f = x / K, c = x - f * K;
     const float v = tab(E, TBF, clamp_id(q[b * F + (f == 0 ? 0 : f + 1)], M), K, c);
     ufs[x] = v;
     Ql[x] = P[c] * v;
-  }
-  for (int x = tid; x < NA; x += 512) {
-    bl[x] = x < A ? att_b[x] : 0.f;
-    apl[x] = x < A ? att_p[x] : 0.f;
   }
   __syncthreads();
   for (int x = tid; x < uF * NA * U2; x += 512) {
@@ -1049,9 +1062,6 @@ __global__ __launch_bounds__(512) void afm_cat_w(
   __syncthreads();
 
   const float ud = ufdot[b], sa = suma[b];
-  const int ntile = (N + 31) / 32;
-  const int t0 = chunk * tiles_per_block;
-  const int t1 = min(t0 + tiles_per_block, ntile);
   // this lane's k of 16-k step t: {16t + 4h .. +3, 16t + 8 + 4h .. +3}
   auto gather = [&](int tile, float (&x)[KS][8]) {
     int32_t item = tile * 32 + j;
@@ -1152,6 +1162,7 @@ __global__ __launch_bounds__(512) void afm_cat_w(
     }
     if (item < N && h == 0)
       scores[b * N + item] = (ud + num) / (sa + den) + w[item_row_begin + item];
+  }
   }
 }
 
@@ -1463,18 +1474,18 @@ extern "C" int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t 
           default: wl = afm_cat_w_lds<4>(F, A); break;
         }
         if (wl <= 160 * 1024) {
-          int64_t nch = (1024 + nq - 1) / nq;
-          const int64_t maxch = ntile / 32 > 1 ? ntile / 32 : 1;   // >= 4 tiles per wave
-          if (nch > maxch) nch = maxch;
-          const int tpw = (int)((ntile + nch - 1) / nch);
-          nch = (ntile + tpw - 1) / tpw;
-          const dim3 wgrid((unsigned)(nq * nch));
+          // one block per CU walks an equal share of the query-major tiles
+          int dev = 0, cus = 256;
+          if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+          const int64_t T = nq * (int64_t)ntile;
+          const dim3 wgrid((unsigned)(T < cus ? T : cus));
 #define HHFM_AFM_CAT_W_L(N, TB, KS)                                                              \
   {                                                                                             \
     allow_lds((const void*)afm_cat_w<TB, N, KS>, wl);                                            \
     hipLaunchKernelGGL((afm_cat_w<TB, N, KS>), wgrid, dim3(512), wl, st, qidx + b0 * F, nq, F,   \
                        E, features_M, Wt, att_b, att_p, A, P, ud, sa, (int64_t)item_row_begin,   \
-                       item_count, tpw, (int)nch, w, sc);                                        \
+                       item_count, w, sc);                                                       \
     wdone = true;                                                                               \
   }
 #define HHFM_AFM_CAT_W_K(N, TB)                                                                  \

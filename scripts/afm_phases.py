@@ -4,6 +4,7 @@ prints one JSON object."""
 import json
 import os
 import sys
+import time
 
 import torch
 
@@ -13,17 +14,22 @@ from hhfm_amd.AFM import AFM  # noqa: E402
 
 
 def timeit(fn, reps=7):
+    """Median device time per call, calls queued back to back (host set-up
+    overlaps the previous call instead of being timed as idle device time)."""
     fn()
     torch.cuda.synchronize()
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_end = time.perf_counter() + 0.2   # >= 200 ms of the same work first: clocks ramp
+    while time.perf_counter() < t_end:
+        fn()
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
         a.record()
         fn()
         b.record()
-        torch.cuda.synchronize()
-        ts.append(a.elapsed_time(b))
-    ts.sort()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
     return round(ts[len(ts) // 2], 4)
 
 

@@ -38,18 +38,24 @@ only = os.environ.get("ROWS_ONLY", "")
 
 
 def gpu_ms(fn, reps=10, warm=2):
+    """Median device time per call, calls queued back to back (no host sync
+    between them, so a call's host-side set-up overlaps the previous call's
+    kernels instead of being timed as idle device time)."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
-    ts = []
-    for _ in range(reps):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t_end = time.perf_counter() + 0.2   # >= 200 ms of the same work first: clocks ramp
+    while time.perf_counter() < t_end:
+        fn()
+        torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in ev:
         a.record()
         fn()
         b.record()
-        b.synchronize()
-        ts.append(a.elapsed_time(b))
-    return float(np.median(ts))
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev]))
 
 
 def cpu_s(fn, budget=3.0):
