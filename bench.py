@@ -884,7 +884,7 @@ def main():
                    "parallelism": f"rows sharded x{world}, no collective"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "fm_rows_fast<5,16,f32,w>", "kernel_ms": kern_ms,
+                     "kernel": "fm_rows_fast<5,16,f32,w,NTM 2>", "kernel_ms": kern_ms,
                      "traffic_GBps": (traffic / (kern_ms * 1e-3) / 1e9) if traffic else None,
                      "traffic_frac": (traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
                                      if traffic else None,

@@ -40,7 +40,13 @@ HHFM_DEV void load_ids(int32_t (&id)[U][F], const int32_t* __restrict__ idx,
 // ---------------------------------------------------------------------------
 // FM row kernel: out = Σ_k ½[(Σ_f e)² − Σ_f e²] + Σ_f w + w0
 // ---------------------------------------------------------------------------
-template <int F, int LPR, bool BF16, bool HAS_W, bool NT>
+// NTM: 0 every load default, 1 every load non-temporal (HHFM_FLAG_STREAM_TABLE),
+// 2 only the user and item rows (fields 0, 1) non-temporal — planned for
+// tables far beyond the caches, where those rows are read once and the
+// default policy lets them evict the re-read `w` lines and context rows from
+// the Infinity Cache: 4.21 -> 4.11 ms at configs[1] (ids and output
+// non-temporal as well: 4.53 ms; profiles/r04_k1_nt_ab.txt)
+template <int F, int LPR, bool BF16, bool HAS_W, int NTM>
 __global__ __launch_bounds__(256) void fm_rows_fast(
     const int32_t* __restrict__ idx, int64_t B, const char* __restrict__ E,
     int64_t M, const float* __restrict__ w, float w0, float* __restrict__ out,
@@ -49,6 +55,7 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
   constexpr int RPW = kWave / LPR;  // rows per wave per unroll slot
   constexpr int RPI = RPW * U;      // rows per wave-iteration
   constexpr int64_t ROW_BYTES = (int64_t)LPR * 16;
+  constexpr bool NT = NTM == 1;
   using C = Chunk<BF16>;
 
   const int lane = threadIdx.x & (kWave - 1);
@@ -72,7 +79,10 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
         bad |= id[u][f] != raw[u][f];
-        c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
+        if (NTM == 2 && f < 2)
+          c[u][f].template load<true>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
+        else
+          c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
       }
 
     // Σ_f w[x_f]: lane `sub` gathers fields f ≡ sub (mod LPR); loads are
@@ -288,14 +298,19 @@ static void launch_fm_fast(const int32_t* idx, int64_t B, const char* E,
                            bool nt, int32_t* status, hipStream_t s) {
   constexpr int RPB = 4 * (kWave / LPR) * RowsPerLane<F>::value;
   const int grid = grid_for(B, RPB);
+  // rows far beyond the caches: the user / item rows streamed (NTM 2)
+  const bool big = M * (int64_t)LPR * 16 >= ((int64_t)1 << 30);
   if (w && nt)
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, true>), dim3(grid),
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, 1>), dim3(grid),
+                       dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
+  else if (w && big && F >= 2)
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, 2>), dim3(grid),
                        dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else if (w)
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, false>), dim3(grid),
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, true, 0>), dim3(grid),
                        dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
   else
-    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, false>), dim3(grid),
+    hipLaunchKernelGGL((fm_rows_fast<F, LPR, BF16, false, 0>), dim3(grid),
                        dim3(256), 0, s, idx, B, E, M, w, w0, out, status);
 }
 

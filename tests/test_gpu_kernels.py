@@ -114,6 +114,44 @@ def test_fm_score_rows_flag_variants_bit_identical(dtype, k, F):
         assert torch.equal(o, outs[0])
 
 
+@pytest.mark.parametrize("k,F", [(64, 5), (128, 3)])
+def test_fm_score_rows_big_table_streamed_rows(k, F):
+    """A table past 1 GiB plans the user / item rows as non-temporal loads
+    (fm_rows_fast NTM 2): the same bits as the all-streaming flag and the
+    default policy's arithmetic, and the oracle's values on the rows used."""
+    from hhfm_amd._native import native
+    rng = np.random.default_rng(99 + k)
+    M = (1 << 30) // (4 * k) + 1000          # just over 1 GiB of fp32 rows
+    B = 8192
+    Xh = rng.integers(0, M, size=(B, F)).astype(np.int32)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(k)
+    E = torch.empty(M, k, device="cuda").normal_(0, 0.05, generator=g)
+    w = torch.empty(M, device="cuda").normal_(0, 0.01, generator=g)
+    X = _dev(Xh)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for flags in (0, 1):
+        o = torch.full((B,), float("nan"), device="cuda")
+        native().fm_score_rows_ex(X.data_ptr(), B, F, E.data_ptr(), M, k, 0, w.data_ptr(),
+                                  0.003, o.data_ptr(), flags, 0, st)
+        outs.append(o.cpu())
+    assert torch.equal(outs[0], outs[1])
+    # oracle on the referenced rows only (re-indexed into a compact table)
+    uniq, inv = np.unique(Xh.reshape(-1), return_inverse=True)
+    ui = torch.from_numpy(uniq.astype(np.int64)).cuda()
+    Eh = E[ui].cpu().numpy()
+    wh = w[ui].cpu().numpy()
+    Xc = inv.reshape(B, F).astype(np.int32)
+    del E, w
+    torch.cuda.empty_cache()
+    got = outs[0].numpy()
+    ref = orc.fm_out(Xc, Eh, wh, 0.003)[:, 0]
+    scale = _fm_scale(Xc, Eh, wh, 0.003)
+    assert np.all(np.abs(got - ref) <= RTOL * scale + 1e-12)
+    _elementwise_vs_exact(got, ref, Xc, Eh, wh, 0.003, scale)
+
+
 @pytest.mark.parametrize("B", [0, 1, 7, 63, 1000])
 def test_fm_score_rows_ragged_and_generic(B):
     """Odd B, and k=20 (not 16-B aligned rows -> generic kernel), no w."""
