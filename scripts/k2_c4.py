@@ -8,6 +8,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -48,14 +49,20 @@ def main():
                                         (2, 5), (0, 0), plan=plan)
             run()
             torch.cuda.synchronize()
-            ts = []
-            for _ in range(a.reps):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t_end = time.perf_counter() + 0.2   # >= 200 ms of this work first: clocks ramp
+            while time.perf_counter() < t_end:
+                run()
+                torch.cuda.synchronize()
+            # calls queued back to back: a call's host set-up overlaps the
+            # previous call's kernels instead of being timed as idle device time
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(a.reps)]
+            for e0, e1 in ev:
                 e0.record()
                 s, i = run()
                 e1.record()
-                e1.synchronize()
-                ts.append(e0.elapsed_time(e1))
+            torch.cuda.synchronize()
+            ts = [e0.elapsed_time(e1) for e0, e1 in ev]
             same = None
             if ref is None:
                 ref = (s.clone(), i.clone())
