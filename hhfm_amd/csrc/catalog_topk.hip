@@ -41,9 +41,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
 #endif
-#ifndef HHFM_SEED_MAX
-#define HHFM_SEED_MAX 32768   // items of the threshold seed, at most
-#endif
+// threshold seed, at most: items and score-matrix floats (fp32 / bf16
+// tables; C4 shard, 1,024 queries: bf16 48 K items 0.96 vs 32 K 0.99 ms, fp32
+// 32 K 1.70 vs 48 K 1.71, 16 K / 8 K seeds 12-24 % slower, 128 K 45 % slower:
+// profiles/r04_k2_seed_ab.txt)
+constexpr int64_t kSeedMax[2] = {32768, 49152};
+constexpr int64_t kSeedBudget[2] = {(int64_t)32 << 20, (int64_t)48 << 20};
 #ifndef HHFM_RING_PAIR
 #define HHFM_RING_PAIR 0   // 1: catalog_ring bf16 with one s_barrier per two tiles (6-slot ring; measured neutral at C4, 1.20 vs 1.21 ms)
 #endif
@@ -895,7 +898,7 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // score with the same MFMA products in the same k order as the selecting
 // kernel (operands swapped: D = Aᵀ-layout), so t is bit-exactly a score the
 // main pass reproduces (tests/test_gpu_kernels.py: seeded == unseeded).
-static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan) {
+static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, bool bf16) {
   Plan p{};
   p.nqb = (int)((B + kQPerBlock - 1) / kQPerBlock);
   p.Bpad = (int64_t)p.nqb * kQPerBlock;
@@ -934,12 +937,12 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan) 
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
   if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
-  // seed: up to 32,768 items and a 128 MiB score matrix, only when the
-  // catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
+  // seed: up to kSeedMax items and a kSeedBudget-float score matrix, only when
+  // the catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
   p.seed_n = 0;
   if (!p.dense && !(plan & HHFM_PLAN_NO_SEED)) {
-    int64_t sn = ((int64_t)32 << 20) / p.Bpad;
-    sn = (sn > HHFM_SEED_MAX ? HHFM_SEED_MAX : sn) & ~int64_t(31);
+    int64_t sn = kSeedBudget[bf16] / p.Bpad;
+    sn = (sn > kSeedMax[bf16] ? kSeedMax[bf16] : sn) & ~int64_t(31);
     if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
   }
   p.off_seed_sc = off;
@@ -1094,7 +1097,10 @@ extern "C" int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count,
                                            size_t* ws_bytes) {
   if (!ws_bytes || B < 0 || item_count < 1 || k < 1 || K < 1 || K > 64)
     return HHFM_EINVAL;
-  *ws_bytes = make_plan(B, item_count, k, K, HHFM_PLAN_DEFAULT).total;   // the largest plan
+  // the largest plan of either table dtype
+  const size_t a = make_plan(B, item_count, k, K, HHFM_PLAN_DEFAULT, false).total;
+  const size_t b = make_plan(B, item_count, k, K, HHFM_PLAN_DEFAULT, true).total;
+  *ws_bytes = a > b ? a : b;
   return HHFM_OK;
 }
 
@@ -1140,7 +1146,7 @@ extern "C" int hhfm_catalog_topk_ex(
   if (!qidx || !E || !top_score || !top_idx) return HHFM_EINVAL;
   if ((reinterpret_cast<uintptr_t>(E) & 15) != 0) return HHFM_EUNSUPPORTED;
 
-  const Plan p = make_plan(B, item_count, k, K, plan);
+  const Plan p = make_plan(B, item_count, k, K, plan, bf16);
   if (!workspace || ws_bytes < p.total) return HHFM_EWORKSPACE;
   char* ws = reinterpret_cast<char*>(workspace);
   float* H = reinterpret_cast<float*>(ws + p.off_H);
