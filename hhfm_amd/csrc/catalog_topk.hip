@@ -47,6 +47,9 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // profiles/r04_k2_seed_ab.txt)
 constexpr int64_t kSeedMax[2] = {32768, 49152};
 constexpr int64_t kSeedBudget[2] = {(int64_t)32 << 20, (int64_t)48 << 20};
+#ifndef HHFM_RING_MAXF
+#define HHFM_RING_MAXF 0   // A/B: 1 = ring tiles without a candidate leave after one ballot
+#endif
 #ifndef HHFM_RING_OVERLAP
 #define HHFM_RING_OVERLAP 0   // A/B: 1 = tile t+1's MFMA chain issued before tile t's selection
 #endif
@@ -744,6 +747,14 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
     const int ibase = tile * kTile;
     uint64_t pm[16];
     if (ibase + kTile <= item_end) {
+#if HHFM_RING_MAXF
+      // the common tile has no candidate: one ballot of the lane's maximum
+      // (a score passes iff it is >= thr, so the max passes iff any does)
+      float mx = acc[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+      if (__ballot(mx >= thr) == 0) return;
+#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) pm[r] = __ballot(acc[r] >= thr);
     } else {
