@@ -47,12 +47,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // profiles/r04_k2_seed_ab.txt)
 constexpr int64_t kSeedMax[2] = {32768, 49152};
 constexpr int64_t kSeedBudget[2] = {(int64_t)32 << 20, (int64_t)48 << 20};
-#ifndef HHFM_RING_MAXF
-#define HHFM_RING_MAXF 0   // A/B: 1 = ring tiles without a candidate leave after one ballot
-#endif
-#ifndef HHFM_RING_OVERLAP
-#define HHFM_RING_OVERLAP 0   // A/B: 1 = tile t+1's MFMA chain issued before tile t's selection
-#endif
 #ifndef HHFM_RING_PAIR
 #define HHFM_RING_PAIR 0   // 1: catalog_ring bf16 with one s_barrier per two tiles (6-slot ring; measured neutral at C4, 1.20 vs 1.21 ms)
 #endif
@@ -681,7 +675,8 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   // one tile: raw sets (cur holds tile+1's unit, nxt receives tile+3's) for fp32
   // sync: publish the stage (every fp32 tile; bf16 pairs: the first tile of
   // each pair, whose barrier also covers the second)
-  auto issue = [&](const int tile, uint4 (&cur)[NUL][2], const bool sync) -> f32x16 {
+  auto tile_step = [&](const int tile, uint4 (&cur)[NUL][2], uint4 (&nxt)[NUL][2],
+                       const bool sync) {
     const int it = tile - tb0;
     // ---- publish: tile's stage complete and the previous tile's stage free ----
     if (sync) {
@@ -706,6 +701,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
         if (tile + 3 < tb1) load_unit(tile + 3, cur);
       }
     }
+    (void)nxt;
     float wcur = wnext;
     if constexpr (FM) {
       const int item = min((tile + 1 < tb1 ? tile + 1 : tile) * kTile + j, N - 1);
@@ -739,22 +735,11 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
     if constexpr (FM)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f, h == 0 ? 1.f : cq, acc,
                                                  0, 0, 0);
-    return acc;
-  };
-  // ---- filter + insert: catalog_main's selection ----
-  auto select = [&](const int tile, const f32x16& acc) {
     if (!wave_live) return;
+    // ---- filter + insert: catalog_main's selection ----
     const int ibase = tile * kTile;
     uint64_t pm[16];
     if (ibase + kTile <= item_end) {
-#if HHFM_RING_MAXF
-      // the common tile has no candidate: one ballot of the lane's maximum
-      // (a score passes iff it is >= thr, so the max passes iff any does)
-      float mx = acc[0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
-      if (__ballot(mx >= thr) == 0) return;
-#endif
 #pragma unroll
       for (int r = 0; r < 16; ++r) pm[r] = __ballot(acc[r] >= thr);
     } else {
@@ -790,27 +775,10 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
       }
     }
   };
-#if HHFM_RING_OVERLAP
-  // software-pipelined: tile t+1's barrier, DMA and MFMA chain are issued
-  // before tile t's selection, so the selection's VALU / SALU work runs under
-  // the next chain instead of between chains (the same products and order)
-  if (tb0 < tb1) {
-    f32x16 acc0 = issue(tb0, rawB, true), acc1;
-    for (int tile = tb0; tile < tb1; tile += 2) {
-      if (tile + 1 < tb1) acc1 = issue(tile + 1, rawA, !kPair);
-      select(tile, acc0);
-      if (tile + 1 < tb1) {
-        if (tile + 2 < tb1) acc0 = issue(tile + 2, rawB, true);
-        select(tile + 1, acc1);
-      }
-    }
-  }
-#else
   for (int tile = tb0; tile < tb1; tile += 2) {
-    select(tile, issue(tile, rawB, true));
-    if (tile + 1 < tb1) select(tile + 1, issue(tile + 1, rawA, !kPair));
+    tile_step(tile, rawB, rawA, true);
+    if (tile + 1 < tb1) tile_step(tile + 1, rawA, rawB, !kPair);
   }
-#endif
 #undef HHFM_VMCNT
   if (!wave_live) return;
   __builtin_amdgcn_s_waitcnt(0xc07f);

@@ -51,11 +51,6 @@ constexpr int kWideRows = 192;
 #ifndef HHFM_WFM
 #define HHFM_WFM 1
 #endif
-// hidden layers: a pass's epilogue issued among the next pass's first MFMA
-// steps (0: after its own chain)
-#ifndef HHFM_WEPI
-#define HHFM_WEPI 0
-#endif
 // staged blocks: P sums of layer-0 pass t+1 among pass t's MFMA steps (0: at
 // the pass start)
 #ifndef HHFM_WPI
@@ -440,54 +435,11 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       }
     };
     f32x4 accN[3][2];
-    f32x4 accs[2][3][2];   // pass p's accumulators: accs[p & 1]
-
-    // pass (layer, t)'s epilogue for row tile rt: ReLU (DFM.py:128) + bf16
-    // into the next layer's B operand, or (last layer) ReLU · concat
-    // projection into part.  Units 32t + 4kq .. +3 and 32t + 16 + 4kq .. +3
-    // are lane group kq's k of step t next layer.  RNE first, then the ReLU
-    // on the packed pair as int16 max with 0 (a negative bf16 is a negative
-    // int16, and RNE keeps the sign): the same bits as rounding max(x, 0)
-    auto epi = [&](auto lc, auto tc, const f32x4 (&acc)[3][2], int rt) {
-      constexpr int layer = decltype(lc)::value, t = decltype(tc)::value;
-      const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
-      if constexpr (layer < 2) {
-        const uint4 o = make_uint4(relu_bf16x2(pack_bf16x2(c0[0], c0[1])),
-                                   relu_bf16x2(pack_bf16x2(c0[2], c0[3])),
-                                   relu_bf16x2(pack_bf16x2(c1[0], c1[1])),
-                                   relu_bf16x2(pack_bf16x2(c1[2], c1[3])));
-        if constexpr (layer == 0)
-          X[rt][t] = o;
-        else
-          Y[rt][t] = o;
-        pin(layer == 0 ? X[rt][t] : Y[rt][t]);
-      } else {
-        const float* vv = vl + 32 * t + 4 * kq;
-        const float4 v0 = *reinterpret_cast<const float4*>(vv);
-        const float4 v1 = *reinterpret_cast<const float4*>(vv + 16);
-        part[rt] += fmaxf(c0[0], 0.f) * v0.x;
-        part[rt] += fmaxf(c0[1], 0.f) * v0.y;
-        part[rt] += fmaxf(c0[2], 0.f) * v0.z;
-        part[rt] += fmaxf(c0[3], 0.f) * v0.w;
-        part[rt] += fmaxf(c1[0], 0.f) * v1.x;
-        part[rt] += fmaxf(c1[1], 0.f) * v1.y;
-        part[rt] += fmaxf(c1[2], 0.f) * v1.z;
-        part[rt] += fmaxf(c1[3], 0.f) * v1.w;
-        pin(part[rt]);
-      }
-    };
 
     static_for<0, NCH>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
       constexpr int layer = p / TM, t = p % TM;
       constexpr int S = layer == 0 ? S0 : TM;
-      // hidden-layer passes but a layer's last defer their epilogue into the
-      // next pass's first three MFMA steps (one row tile per step: its VALU
-      // issues under that step's MFMAs instead of between two chains)
-      constexpr bool DEFER = HHFM_WEPI && layer >= 1 && t + 1 < TM;
-      constexpr bool PREV = HHFM_WEPI && layer >= 1 && t >= 1;   // pass p-1 deferred its epilogue
-      using PL = std::integral_constant<int, layer>;
-      using PT = std::integral_constant<int, (t >= 1 ? t - 1 : 0)>;
       constexpr int Unext = p + 1 < NCH ? (p + 1 < TM ? 2 * S0 : 2 * TM) : 0;
       if constexpr (p > 0 && !(HHFM_WKO & 4)) vm_barrier<Unext / 4>();   // pass p landed; slot (p+2)%3 free
       const uint4* wsl = reinterpret_cast<const uint4*>(smem + (p % 3) * kSlotB) + l;
@@ -500,7 +452,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       const f32x4 binit[2] = {*reinterpret_cast<const f32x4*>(bl),
                               *reinterpret_cast<const f32x4*>(bl + 16)};
       constexpr bool PI = ST && HHFM_WPI && !(HHFM_WKO & 2);   // interleaved P sums
-      f32x4 (&acc)[3][2] = accs[p & 1];
+      f32x4 acc[3][2];
       if constexpr (layer == 0 && PI && t > 0) {
 #pragma unroll
         for (int rt = 0; rt < 3; ++rt)
@@ -559,8 +511,6 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
 #endif
         }
         if constexpr (PN) psum_part(t + 1, s, accN);
-        if constexpr (PREV)
-          if (s < 3) epi(PL{}, PT{}, accs[(p + 1) & 1], s);
         if (dq < Udma) {
           dma_unit(p + 2, dq);
           dq += 4;
@@ -571,9 +521,42 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         dma_unit(p + 2, dq);
         dq += 4;
       }
-      if constexpr (!DEFER) {
+      if constexpr (layer < 2) {
+        // ReLU (DFM.py:128) + bf16: units 32t + 4kq .. +3 and 32t + 16 + 4kq
+        // .. +3 are lane group kq's k of step t next layer.  RNE first, then
+        // the ReLU on the packed pair as int16 max with 0 (a negative bf16 is
+        // a negative int16, and RNE keeps the sign): the same bits as
+        // rounding max(x, 0)
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) epi(PL{}, std::integral_constant<int, t>{}, acc, rt);
+        for (int rt = 0; rt < 3; ++rt) {
+          const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
+          const uint4 o = make_uint4(relu_bf16x2(pack_bf16x2(c0[0], c0[1])),
+                                     relu_bf16x2(pack_bf16x2(c0[2], c0[3])),
+                                     relu_bf16x2(pack_bf16x2(c1[0], c1[1])),
+                                     relu_bf16x2(pack_bf16x2(c1[2], c1[3])));
+          if constexpr (layer == 0)
+            X[rt][t] = o;
+          else
+            Y[rt][t] = o;
+          pin(layer == 0 ? X[rt][t] : Y[rt][t]);
+        }
+      } else {
+        const float* vv = vl + 32 * t + 4 * kq;
+        const float4 v0 = *reinterpret_cast<const float4*>(vv);
+        const float4 v1 = *reinterpret_cast<const float4*>(vv + 16);
+#pragma unroll
+        for (int rt = 0; rt < 3; ++rt) {
+          const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
+          part[rt] += fmaxf(c0[0], 0.f) * v0.x;
+          part[rt] += fmaxf(c0[1], 0.f) * v0.y;
+          part[rt] += fmaxf(c0[2], 0.f) * v0.z;
+          part[rt] += fmaxf(c0[3], 0.f) * v0.w;
+          part[rt] += fmaxf(c1[0], 0.f) * v1.x;
+          part[rt] += fmaxf(c1[1], 0.f) * v1.y;
+          part[rt] += fmaxf(c1[2], 0.f) * v1.z;
+          part[rt] += fmaxf(c1[3], 0.f) * v1.w;
+          pin(part[rt]);
+        }
       }
     });
 
