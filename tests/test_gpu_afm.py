@@ -148,6 +148,8 @@ def test_afm_rows_envelope(F, k, A, tdt, B):
     (5, 48, 48, "f32", 17, 901, 20),      # per-query kernel at k = 48 (U2 = 6 swizzle)
     (3, 48, 40, "f32", 33, 777, 20),      # ... A padded to 64, two query fields
     (5, 32, 96, "f32", 9, 555, 20),       # A = 96: 32-column logit groups on the GEMM path
+    (5, 64, 64, "f32", 1, 100, 10),       # persistent per-query kernel: 4 tiles, grid of 4
+    (5, 32, 32, "bf16", 3, 70, 5),        # ... 3 queries x 3 tiles: shares cross queries
 ])
 def test_afm_catalog_envelope(F, k, A, tdt, nq, ni, K):
     """A2 across the fused kernels' envelope (the per-query kernel with the
