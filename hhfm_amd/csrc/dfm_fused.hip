@@ -992,6 +992,29 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     phi[tid] = -1;
   }
   __syncthreads();
+  const int myrow = 16 * wv + r;
+  f32x4 X[T16];
+  // field 1 (the item: its ids span the whole catalog, it is never staged)
+  // is gathered into X now, in flight through the span / staging prologue;
+  // X = P_1 + P_0 + P_2 + ... equals the in-order sum bit for bit (IEEE
+  // addition commutes, and 0 + P_0 = P_0); C5 fp32 38.84 -> 38.70 ms
+  // (profiles/r04_k3_f32_pre_ab.txt)
+  constexpr int kPre = 1;
+  const bool pre = F > kPre;
+  if (pre) {
+    const int id = ids[myrow * F + kPre];
+    const float4* pp = reinterpret_cast<const float4*>(
+                           reinterpret_cast<const float*>(a.proj) + kPre * a.proj_fstride +
+                           (int64_t)id * a.proj_ld) + kq;
+#pragma unroll
+    for (int t = 0; t < T16; ++t) {
+      const float4 x = pp[4 * t];
+      X[t] = f32x4{x.x, x.y, x.z, x.w};
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < T16; ++t) X[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   // each field's id span over the block (rows grouped by user: the user and
   // the context fields span a few table rows)
   for (int x = tid; x < Cfg::kRows * F; x += NT) {
@@ -1007,7 +1030,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   int staged = 0;
   for (int f = 0; f < F; ++f) {
     const int span = phi[f] - plo[f] + 1;
-    const bool st = a.stage && span > 0 && staged + span <= kStageRows;
+    const bool st = a.stage && f != kPre && span > 0 && staged + span <= kStageRows;
     if (tid == 0) psb[f] = st ? staged : -1;
     staged += st ? span : 0;
   }
@@ -1054,11 +1077,8 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
 
   // ----- layer 0 from P: X = Σ_f P_f[x_f] (lane group kq: units 16t+4kq..+3),
   // straight into the registers of layer 1's input -----
-  const int myrow = 16 * wv + r;
-  f32x4 X[T16];
-#pragma unroll
-  for (int t = 0; t < T16; ++t) X[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int f = 0; f < F; ++f) {
+    if (f == kPre) continue;   // already in X
     const int id = ids[myrow * F + f];
     const int sb = psb[f];   // uniform: this field's rows staged in LDS
     if (sb >= 0) {
