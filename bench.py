@@ -583,9 +583,9 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
                             f"Frappe vocabulary, rows sharded {rows:,} per GPU", "ranks": world,
                 "rows_per_s": rows * world / (ms * 1e-3), "ms_per_pass": ms, "kernel_ms": kern,
                 "executed_TFLOPs": ex / (kern * 1e-3) / 1e12,
-                "kernel": "dfm_fused_w<13,8,4,true> (dfm_wide.hip: 192 rows per workgroup, 48 "
-                          "per wave) after the user grouping, the projection, the FM pair table "
-                          "and the weight packing",
+                "kernel": "dfm_fused_w<13,8,4,true,2,8> (dfm_wide.hip: 256 rows per workgroup, "
+                          "32 per wave, two waves per SIMD) after the user grouping, the "
+                          "projection, the FM pair table and the weight packing",
                 "roofline": {"bound": "mfma", "executed_flops_per_pass": ex,
                              "achieved_TFLOPs": ex / (kern * 1e-3) / 1e12,
                              "peak_TFLOPs": 2500.0,

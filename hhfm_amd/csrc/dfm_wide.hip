@@ -9,20 +9,23 @@
 namespace hhfm {
 
 // ---------------------------------------------------------------------------
-// K3w — the bf16-MLP DeepFM forward at 192 rows per workgroup (the ITEM plan:
+// K3w — the bf16-MLP DeepFM forward at 256 rows per workgroup (the ITEM plan:
 // layer 0 of the item field on MFMA, every other field from P, rows grouped
 // by user).  dfm_fused keeps 32 rows x all output units per wave in
 // accumulators (208 registers), so its workgroup holds 128 rows and streams
 // every weight once per 128 rows: ≈32 B/clk of L2 -> LDS per CU at the MFMA
 // rate, what one CU pulls — the C5 kernel ran at that stream, MFMA busy 35 %.
-// Here a wave owns 48 rows (three 16-row tiles, v_mfma_f32_16x16x32_bf16) and
+// Here a wave owns RT 16-row tiles (v_mfma_f32_16x16x32_bf16; RT = 2 at two
+// waves per SIMD, 8 waves = 256 rows, by default; RT = 3 at one, 192 rows) and
 // walks the output units 32 at a time: per pass, the full-K MFMA chain of
 // 2 unit tiles x 3 row tiles (24 accumulator registers), then bias + ReLU +
 // bf16 straight into the next layer's B operand — the 16x16 result puts
 // units 4kq..+3 of a tile on lane group kq, exactly the k a lane group
 // supplies next (k order {32s + 4kq .. +3, 32s + 16 + 4kq .. +3}), so no
-// lane movement.  Live: the layer input (156 registers for 48 rows x 416
-// units) + the output being built (156) + 24, at one wave per SIMD; the
+// lane movement.  Live: the layer input (104 registers for 32 rows x 416
+// units) + the output being built (104) + 16 (RT = 2; the compiler spills
+// ~56 registers of the prologue's state at the 256 two waves per SIMD
+// leave, measured faster all the same); the
 // weight stream per row falls to 2/3 (≈21 B/clk per CU), each 1-KB A
 // fragment feeds three MFMAs.
 //   * weights: dfm_pack_weights_w lays each (layer, 32-unit pass) out as S
@@ -38,13 +41,23 @@ namespace hhfm {
 // Instantiated per shape (TM 32-unit passes in every layer, S0 = k/32 item
 // steps, NF projected fields); other shapes take dfm_fused.
 // ---------------------------------------------------------------------------
-constexpr int kWideRows = 192;
 
 // diagnostic knock-outs (timing only, wrong results; default 0): 1 FM part,
 // 2 P sums, 4 per-pass barriers, 8 weight DMA after the first two passes,
 // 16 MFMAs, 32 staging copies
 #ifndef HHFM_WKO
 #define HHFM_WKO 0
+#endif
+// 16-row tiles per wave and waves per workgroup: 2 x 8 = 256 rows, two waves
+// per SIMD (C5 bf16 10.0-10.3 ms, bit-identical), against 3 x 4 = 192 rows at
+// one wave per SIMD (12.9-13.0 ms; profiles/r04_k3w_two_waves_ab.txt): the
+// second wave's MFMAs cover the first's DMA issue, epilogue and barrier waits,
+// and each weight byte streamed feeds 256 rows instead of 192
+#ifndef HHFM_WIDE_RT
+#define HHFM_WIDE_RT 2
+#endif
+#ifndef HHFM_WIDE_NWV
+#define HHFM_WIDE_NWV 8
 #endif
 // FM part of staged blocks: the fields' Σ_k Wp_k·e_k² from per-row sums g
 // computed once per staged table row (0: per row and k, as unstaged blocks)
@@ -147,8 +160,12 @@ __global__ __launch_bounds__(256) void dfm_pack_weights_w(FusedDfmArgs a, int TM
   }
 }
 
-template <int TM, int S0, int NF, bool PAIRS>
-__global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
+// RT row tiles (16 rows) per wave, NWV waves: 3 x 4 (one wave per SIMD,
+// 192 rows) or 2 x 8 (two waves per SIMD, 256 rows)
+template <int TM, int S0, int NF, bool PAIRS, int RT = 3, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
+  constexpr int kWideRows = NWV * 16 * RT;
+  constexpr int NTH = NWV * 64;
   // PAIRS: a.fmbase[m] = (Σ_f w·Wp + FM part) + bp from the pair table
   // (dfm_fm_pairs), so no table rows are staged and no FM part runs here
   static_assert(NF >= 1 && NF < kFusedMaxF, "wide DeepFM kernel: fields");
@@ -186,16 +203,16 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   const uint16_t* E = reinterpret_cast<const uint16_t*>(a.E);
 
   // rows past B repeat row B-1 (never stored), so the id spans stay tight
-  for (int x = tid; x < kWideRows * F; x += 256) {
+  for (int x = tid; x < kWideRows * F; x += NTH) {
     int64_t m = m0 + x / F;
     m = m < a.B ? m : a.B - 1;
     const int fe = (int)((a.perm >> (4 * (x % F))) & 15);
     ids[x] = clamp_id(a.idx[m * F + fe], a.M);
   }
   for (int i = 0; i < 3; ++i)
-    for (int n = tid; n < NR; n += 256) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
-  for (int n = tid; n < NR; n += 256) vl[n] = n < a.dims[2] ? a.Wp[F + k + n] : 0.f;
-  for (int x = tid; x < F + k; x += 256)
+    for (int n = tid; n < NR; n += NTH) blv[i * NR + n] = n < a.dims[i] ? a.bias[i][n] : 0.f;
+  for (int n = tid; n < NR; n += NTH) vl[n] = n < a.dims[2] ? a.Wp[F + k + n] : 0.f;
+  for (int x = tid; x < F + k; x += NTH)
     wpl[x < F ? x : x - F + kFusedMaxF] = a.Wp[x < F ? (int)((a.perm >> (4 * x)) & 15) : x];
   if (tid < kFusedMaxF) {
     plo[tid] = 0x7fffffff;
@@ -210,14 +227,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     dma16_at(a.packed + (int64_t)(cbase(c) + u) * 64 + l, lds0 + (c % 3) * kSlotB + u * 1024);
   };
   for (int c = 0; c < 2; ++c)
-    for (int u = wv; u < cunits(c); u += 4) dma_unit(c, u);
+    for (int u = wv; u < cunits(c); u += NWV) dma_unit(c, u);
 
   // layer 0's B operand: the item rows of this lane's three rows (k32 step
   // s: columns 32s + 8kq .. +7), in flight with the weight passes
-  const int row0 = 48 * wv + r;            // row tile rt: row0 + 16·rt
-  uint4 E0[3][S0];
+  const int row0 = 16 * RT * wv + r;       // row tile rt: row0 + 16·rt
+  uint4 E0[RT][S0];
 #pragma unroll
-  for (int rt = 0; rt < 3; ++rt) {
+  for (int rt = 0; rt < RT; ++rt) {
     const int64_t id = ids[(row0 + 16 * rt) * F];
 #pragma unroll
     for (int s = 0; s < S0; ++s)
@@ -233,7 +250,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       if (f < F) y1 += wv8[f] * wpl[f];
     ylds[tid] = y1;
   }
-  for (int x = tid; x < kWideRows * NF; x += 256) {
+  for (int x = tid; x < kWideRows * NF; x += NTH) {
     const int row = x / NF, f = 1 + x % NF;
     atomicMin(&plo[f], ids[row * F + f]);
     atomicMax(&plo[kFusedMaxF + f], ids[row * F + f]);
@@ -266,7 +283,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     int used = 0;
     for (int f = 1; f < F; ++f) {
       const int lo = plo[f], span = plo[kFusedMaxF + f] - lo + 1;
-      for (int x = tid; x < span * (NR / 4); x += 256) {
+      for (int x = tid; x < span * (NR / 4); x += NTH) {
         const int row = x / (NR / 4), c4 = x % (NR / 4);
         *reinterpret_cast<float4*>(pst + used + row * kPsLd + 4 * c4) =
             *reinterpret_cast<const float4*>(P + (f - 1) * a.proj_fstride +
@@ -280,7 +297,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       // consecutive lanes of one wave, summed by a butterfly
       constexpr int CPR = 4 * S0;   // 16-B chunks per bf16 row (k = 32·S0)
       static_assert((CPR & (CPR - 1)) == 0 && CPR <= kWave, "wide DeepFM kernel: k");
-      for (int x = tid; x < (PAIRS ? 0 : span * CPR); x += 256) {
+      for (int x = tid; x < (PAIRS ? 0 : span * CPR); x += NTH) {
         const int row = x / CPR, c = x % CPR;
         const float4 v = Ef[x];
         dst[row * (ekp / 4) + c] = v;
@@ -309,24 +326,24 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
   auto body = [&](auto stc) {
     constexpr bool ST = decltype(stc)::value;
     // layer inputs in B-operand form, one uint4 per (row tile, k32 step)
-    uint4 X[3][TM], Y[3][TM];
-    float y2[3] = {0.f, 0.f, 0.f}, part[3] = {0.f, 0.f, 0.f};
-    int pid[3][F];   // this lane's rows' ids (projected fields)
+    uint4 X[RT][TM], Y[RT][TM];
+    float y2[RT] = {}, part[RT] = {};
+    int pid[RT][F];   // this lane's rows' ids (projected fields)
 #pragma unroll
-    for (int rt = 0; rt < 3; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int f = 1; f < F; ++f) pid[rt][f] = ids[(row0 + 16 * rt) * F + f];
     // staged blocks: LDS float offsets of the rows' P and table rows, and
     // ½ Σ_f g[x_f] of the rows (lane group 0 adds it at the end)
-    int pb[3][F], eb[3][F];
-    float gh[3] = {0.f, 0.f, 0.f};
+    int pb[RT][F], eb[RT][F];
+    float gh[RT] = {};
     if constexpr (ST) {
 #pragma unroll
       for (int f = 1; f < F; ++f) {
         const int lo = plo[f], pofs = plo[2 * kFusedMaxF + f], eofs = plo[3 * kFusedMaxF + f];
         const int gofs = plo[4 * kFusedMaxF + f];
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           pb[rt][f] = pofs + (pid[rt][f] - lo) * kPsLd;
           eb[rt][f] = eofs + (pid[rt][f] - lo) * ekp;
           if constexpr (HHFM_WFM && !PAIRS) gh[rt] += pst[gofs + pid[rt][f] - lo];
@@ -340,7 +357,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
 #pragma unroll
     for (int s = 0; s < ((HHFM_WKO & 1) || PAIRS ? 0 : S0); ++s) {
 #pragma unroll
-      for (int rt = 0; rt < 3; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
         const uint4 ex = E0[rt][s];
         const uint32_t x4[4] = {ex.x, ex.y, ex.z, ex.w};
         float fs[8], fq[8];
@@ -390,12 +407,12 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
 
     // P_f rows of this lane's three rows, units 32t + 16j + 4kq .. +3 (at
     // dfm_proj_pos of the first: 4 contiguous floats), summed into acc
-    auto psum = [&](int t, f32x4 (&acc)[3][2]) {
+    auto psum = [&](int t, f32x4 (&acc)[RT][2]) {
       const int pos0 = 32 * t + 16 * (kq & 1) + 4 * (kq >> 1);   // j = 0; j = 1: +8
 #pragma unroll
       for (int f = 1; f < F; ++f) {
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           const float* pp;
           if constexpr (ST)
             pp = pst + pb[rt][f] + pos0;
@@ -416,13 +433,13 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     // staged blocks: the P sums of layer-0 pass t+1 are formed during pass t's
     // MFMA steps, unit (field f, row tile rt) in f-major order spread over the
     // steps — per accumulator the same order of additions as psum
-    constexpr int kPU = NF * 3;
-    auto psum_part = [&](int t, int s, f32x4 (&acc)[3][2]) {
+    constexpr int kPU = NF * RT;
+    auto psum_part = [&](int t, int s, f32x4 (&acc)[RT][2]) {
       const int pos0 = 32 * t + 16 * (kq & 1) + 4 * (kq >> 1);
 #pragma unroll
       for (int u = 0; u < kPU; ++u) {
         if (u < s * kPU / S0 || u >= (s + 1) * kPU / S0) continue;
-        const int f = 1 + u / 3, rt = u % 3;
+        const int f = 1 + u / RT, rt = u % RT;
         const float* pp = pst + pb[rt][f] + pos0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -434,14 +451,14 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         }
       }
     };
-    f32x4 accN[3][2];
+    f32x4 accN[RT][2];
 
     static_for<0, NCH>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
       constexpr int layer = p / TM, t = p % TM;
       constexpr int S = layer == 0 ? S0 : TM;
       constexpr int Unext = p + 1 < NCH ? (p + 1 < TM ? 2 * S0 : 2 * TM) : 0;
-      if constexpr (p > 0 && !(HHFM_WKO & 4)) vm_barrier<Unext / 4>();   // pass p landed; slot (p+2)%3 free
+      if constexpr (p > 0 && !(HHFM_WKO & 4)) vm_barrier<Unext / NWV>();   // pass p landed; slot (p+2)%3 free
       const uint4* wsl = reinterpret_cast<const uint4*>(smem + (p % 3) * kSlotB) + l;
       // this wave's DMAs of pass p+2: units wv, wv+4, ..., one per MFMA step
       const int Udma = p + 2 < NCH && !(HHFM_WKO & 8) ? cunits(p + 2) : 0;
@@ -452,15 +469,15 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       const f32x4 binit[2] = {*reinterpret_cast<const f32x4*>(bl),
                               *reinterpret_cast<const f32x4*>(bl + 16)};
       constexpr bool PI = ST && HHFM_WPI && !(HHFM_WKO & 2);   // interleaved P sums
-      f32x4 acc[3][2];
+      f32x4 acc[RT][2];
       if constexpr (layer == 0 && PI && t > 0) {
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[rt][j] = accN[rt][j];
       } else {
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[rt][j] = binit[j];
         if constexpr (layer == 0 && !(HHFM_WKO & 2)) psum(t, acc);
@@ -471,7 +488,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         const f32x4 bnext[2] = {*reinterpret_cast<const f32x4*>(bn),
                                 *reinterpret_cast<const f32x4*>(bn + 16)};
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt)
+        for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
           for (int j = 0; j < 2; ++j) accN[rt][j] = bnext[j];
       }
@@ -479,21 +496,27 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
       // ahead: 12.87-12.93 vs 12.80-12.83 ms at C5, profiles/r04_k3w_wpf_ab.txt)
       uint4 fa0 = wsl[0], fa1 = wsl[64];
       uint4 fb0 = fa0, fb1 = fa1;
-      if (S > 1) {
+      constexpr bool PF2 = RT == 3;   // two waves per SIMD: the other wave covers the LDS latency
+      if (PF2 && S > 1) {
         fb0 = wsl[128];
         fb1 = wsl[192];
       }
 #pragma unroll
       for (int s = 0; s < S; ++s) {
         const bf16x8 a0 = __builtin_bit_cast(bf16x8, fa0), a1 = __builtin_bit_cast(bf16x8, fa1);
-        fa0 = fb0;
-        fa1 = fb1;
-        if (s + 2 < S) {
-          fb0 = wsl[128 * (s + 2)];
-          fb1 = wsl[128 * (s + 2) + 64];
+        if constexpr (PF2) {
+          fa0 = fb0;
+          fa1 = fb1;
+          if (s + 2 < S) {
+            fb0 = wsl[128 * (s + 2)];
+            fb1 = wsl[128 * (s + 2) + 64];
+          }
+        } else if (s + 1 < S) {
+          fa0 = wsl[128 * (s + 1)];
+          fa1 = wsl[128 * (s + 1) + 64];
         }
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           uint4 bx;
           if constexpr (layer == 0)
             bx = E0[rt][s];
@@ -513,13 +536,13 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         if constexpr (PN) psum_part(t + 1, s, accN);
         if (dq < Udma) {
           dma_unit(p + 2, dq);
-          dq += 4;
+          dq += NWV;
         }
         __builtin_amdgcn_sched_barrier(0);   // keep the next fragment reads behind this step
       }
       while (dq < Udma) {
         dma_unit(p + 2, dq);
-        dq += 4;
+        dq += NWV;
       }
       if constexpr (layer < 2) {
         // ReLU (DFM.py:128) + bf16: units 32t + 4kq .. +3 and 32t + 16 + 4kq
@@ -528,7 +551,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         // a negative int16, and RNE keeps the sign): the same bits as
         // rounding max(x, 0)
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
           const uint4 o = make_uint4(relu_bf16x2(pack_bf16x2(c0[0], c0[1])),
                                      relu_bf16x2(pack_bf16x2(c0[2], c0[3])),
@@ -545,7 +568,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
         const float4 v0 = *reinterpret_cast<const float4*>(vv);
         const float4 v1 = *reinterpret_cast<const float4*>(vv + 16);
 #pragma unroll
-        for (int rt = 0; rt < 3; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           const f32x4 c0 = acc[rt][0], c1 = acc[rt][1];
           part[rt] += fmaxf(c0[0], 0.f) * v0.x;
           part[rt] += fmaxf(c0[1], 0.f) * v0.y;
@@ -561,7 +584,7 @@ __global__ __launch_bounds__(256, 1) void dfm_fused_w(FusedDfmArgs a) {
     });
 
 #pragma unroll
-    for (int rt = 0; rt < 3; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
       float pt = part[rt], yy = y2[rt];
       pt += __shfl_xor(pt, 16, kWave);
       pt += __shfl_xor(pt, 32, kWave);
@@ -585,7 +608,9 @@ bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st) {
   for (int i = 0; i < 3; ++i) ok = ok && (a.dims[i] + 31) / 32 == TM;
   if (!ok) return false;
   const int S0 = a.k / 32;
-  const dim3 grid((unsigned)((a.B + kWideRows - 1) / kWideRows));
+  constexpr int kRT = HHFM_WIDE_RT, kNWV = HHFM_WIDE_NWV;
+  constexpr int kRowsWG = kNWV * 16 * kRT;
+  const dim3 grid((unsigned)((a.B + kRowsWG - 1) / kRowsWG));
   const int64_t units = ((int64_t)TM * S0 * 2 + 2 * (int64_t)TM * TM * 2) * 64;
   const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
   uint4* packed = const_cast<uint4*>(a.packed);
@@ -595,9 +620,9 @@ bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st) {
     if (dfm_fm_pairs(a, true, st)) {                                                       \
       FusedDfmArgs b = a;                                                                  \
       b.fmbase = a.fm_out;                                                                 \
-      hipLaunchKernelGGL((dfm_fused_w<T, A, N, true>), grid, dim3(256), 0, st, b);         \
+      hipLaunchKernelGGL((dfm_fused_w<T, A, N, true, kRT, kNWV>), grid, dim3(kNWV * 64), 0, st, b);         \
     } else {                                                                               \
-      hipLaunchKernelGGL((dfm_fused_w<T, A, N, false>), grid, dim3(256), 0, st, a);        \
+      hipLaunchKernelGGL((dfm_fused_w<T, A, N, false, kRT, kNWV>), grid, dim3(kNWV * 64), 0, st, a);        \
     }                                                                                      \
     return true;                                                                           \
   }
