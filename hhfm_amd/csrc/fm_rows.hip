@@ -18,9 +18,16 @@
 
 namespace hhfm {
 
+#ifndef HHFM_K1_U5
+#define HHFM_K1_U5 5   // rows per lane in flight at F = 5
+#endif
+// F = 5 (configs[1]): 5 rows in flight per lane 3.98 ms against 4 4.11, 3
+// 4.07, 6 5.05 (profiles/r04_k1_rows_in_flight_ab.txt); the HHFM rows and
+// the bf16 tables gain or hold too (profiles/r04_k1_u5_microbench.txt)
 template <int F>
 struct RowsPerLane {
-  static constexpr int value = F <= 3 ? 6 : (F <= 5 ? 4 : (F <= 8 ? 3 : 2));
+  static constexpr int value =
+      F <= 3 ? 6 : (F == 4 ? 4 : (F == 5 ? HHFM_K1_U5 : (F <= 8 ? 3 : 2)));
 };
 
 // Raw (unclamped) index rows: nothing may consume them until the gathers
