@@ -18,6 +18,12 @@
 
 namespace hhfm {
 
+// blocks per CU the grid is capped at (grid-stride beyond): at configs[1]
+// 16 / 32 / 64 / 256 / 2048 ran 3.98 / 3.95 / 3.94 / 4.11 / 4.51 ms
+// (profiles/r04_k1_grid_cap_ab.txt)
+#ifndef HHFM_K1_CAP
+#define HHFM_K1_CAP 64
+#endif
 #ifndef HHFM_K1_U5
 #define HHFM_K1_U5 5   // rows per lane in flight at F = 5
 #endif
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(256) void hybrid_rows_generic(
 // ---------------------------------------------------------------------------
 static int grid_for(int64_t rows, int64_t rows_per_block) {
   int64_t g = (rows + rows_per_block - 1) / rows_per_block;
-  const int64_t cap = 256 * 16;  // 256 CUs x 16 blocks; grid-stride the rest
+  const int64_t cap = 256 * HHFM_K1_CAP;  // 256 CUs x HHFM_K1_CAP blocks; grid-stride the rest
   if (g > cap) g = cap;
   if (g < 1) g = 1;
   return (int)g;
