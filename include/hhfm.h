@@ -57,7 +57,7 @@ enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 #define HHFM_PLAN_UNSTAGED (1 << 6)   /* DeepFM fp32 MLP: P rows and table rows read
                                          through the caches, not staged in LDS */
 #define HHFM_PLAN_UNGROUPED (1 << 7)  /* DeepFM fp32 MLP: rows not grouped by user */
-#define HHFM_PLAN_NARROW (1 << 8)     /* DeepFM bf16 ITEM plan: 128-row kernel, not 192 */
+#define HHFM_PLAN_NARROW (1 << 8)     /* DeepFM bf16 ITEM plan: 128-row kernel, not the 256-row one */
 #define HHFM_PLAN_PER_FIELD (1 << 9)  /* AFM catalog: pair product split per query field
                                          (afm_cat_fused), not the folded weights */
 #define HHFM_PLAN_ONE_WAVE (1 << 10)  /* dense top-K: one wave per query at every size */
