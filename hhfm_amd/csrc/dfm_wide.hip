@@ -496,7 +496,11 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       // ahead: 12.87-12.93 vs 12.80-12.83 ms at C5, profiles/r04_k3w_wpf_ab.txt)
       uint4 fa0 = wsl[0], fa1 = wsl[64];
       uint4 fb0 = fa0, fb1 = fa1;
+#ifdef HHFM_WIDE_PF2
+      constexpr bool PF2 = HHFM_WIDE_PF2;
+#else
       constexpr bool PF2 = RT == 3;   // two waves per SIMD: the other wave covers the LDS latency
+#endif
       if (PF2 && S > 1) {
         fb0 = wsl[128];
         fb1 = wsl[192];

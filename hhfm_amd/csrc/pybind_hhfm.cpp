@@ -395,6 +395,19 @@ PYBIND11_MODULE(_hhfm, m) {
           return ws;
         });
 
+  m.def("dfm_train_state_bytes", [](int F, int k, int64_t M, std::vector<int32_t> dims) {
+    size_t n = 0;
+    check(hhfm_dfm_train_state_bytes(F, k, M, (int)dims.size(), dims.data(), &n),
+          "hhfm_dfm_train_state_bytes");
+    return n;
+  });
+
+  m.def("afm_train_state_bytes", [](int F, int k, int A, int64_t M) {
+    size_t n = 0;
+    check(hhfm_afm_train_state_bytes(F, k, A, M, &n), "hhfm_afm_train_state_bytes");
+    return n;
+  });
+
   m.def("dfm_train_step",
         [](uptr idx, uptr y, int64_t B, int F, uptr E, uptr w, int64_t M, int k,
            std::vector<int32_t> dims, std::vector<uptr> W, std::vector<uptr> bias, uptr Wp,

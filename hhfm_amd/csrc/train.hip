@@ -20,6 +20,8 @@
 // accumulates Σ var² of the pre-update table for the reported loss (TF
 // evaluates `loss` and the update in the same run).
 // Gradients of reduce_max split equally between tied maxima (TF _MaxGrad).
+#include <cfloat>
+
 #include "gemm_mfma.h"
 
 namespace hhfm {
@@ -28,7 +30,10 @@ enum { OPT_ADAGRAD = 0, OPT_SGD = 1 };
 constexpr int kMaxNeg = 16;   // negatives per row (the reference samples 10, OurModel7.py:371)
 
 // scal[0] = Σ dL/d(w0)  scal[1] = data loss  scal[2] = Σ E² (pre-update)  scal[3] = Σ w² (unused)
-// scal[8], scal[9] = Adam's β1^t, β2^t (kept between steps; 0 = not started)
+// scal[8], scal[9] = Adam's β1^t, β2^t (kept between steps); scal[10] != 0 once
+// Adam has taken a step (a separate flag: β1^t underflows to exactly 0 after
+// 828 steps (TF's flush-to-zero), and TF then keeps using 0, so 0 cannot also
+// mean "not started")
 __global__ __launch_bounds__(256) void fm_train_rows(
     const int32_t* __restrict__ idx, const float* __restrict__ y, int64_t B, int F,
     const float* __restrict__ E, const float* __restrict__ w, const float* __restrict__ w0,
@@ -156,14 +161,15 @@ __global__ __launch_bounds__(256) void hhfm_train_rows(
 //             var update — the two differ only in rounding
 // g = grad + λ·var; Σ var² (pre-update) accumulated into *sumsq when given.
 // state: Adagrad / Momentum n floats, Adam 2n (m, then v).  pw: the step's
-// β1^t, β2^t (TF's beta1_power / beta2_power; 0 = the first step: β1, β2).
+// β1^t, β2^t (TF's beta1_power / beta2_power) and the started flag pw[2]
+// (0 = the first step, whose powers are β1, β2).
 enum { OPT_MOMENTUM = 2, OPT_ADAM = 3 };
 constexpr float kMomentum = 0.95f, kBeta1 = 0.9f, kBeta2 = 0.999f, kAdamEps = 1e-8f;
 
 struct OptStep {
   int opt;
   float lr;
-  const float* pw;         // Adam: [β1^t, β2^t] (device)
+  const float* pw;         // Adam: [β1^t, β2^t, started] (device)
   const uint8_t* touched;  // sparse Momentum: rows the batch touched (else null)
   int rowlen;              // elements per row of the variable (touched index = i / rowlen)
   int sparse;              // the variable's TF gradient is an IndexedSlices
@@ -176,8 +182,9 @@ __global__ __launch_bounds__(256) void optimizer_apply(float* __restrict__ var,
                                                        float* __restrict__ sumsq) {
   float alpha = 0.f;
   if (o.opt == OPT_ADAM) {
-    const float b1p = o.pw[0] != 0.f ? o.pw[0] : kBeta1;
-    const float b2p = o.pw[1] != 0.f ? o.pw[1] : kBeta2;
+    const bool started = o.pw[2] != 0.f;
+    const float b1p = started ? o.pw[0] : kBeta1;
+    const float b2p = started ? o.pw[1] : kBeta2;
     alpha = o.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   }
   float ss = 0.f;
@@ -219,10 +226,17 @@ __global__ __launch_bounds__(256) void optimizer_apply(float* __restrict__ var,
   }
 }
 
-// after every variable's update: β1^t, β2^t -> β1^(t+1), β2^(t+1) (AdamOptimizer._finish)
+// after every variable's update: β1^t, β2^t -> β1^(t+1), β2^(t+1) (AdamOptimizer._finish).
+// TF runs the product with flush-to-zero set (its CPU thread pools set FTZ/DAZ,
+// core/lib/core/threadpool.cc), so β1^t reaches exactly 0 at t = 829 and stays
+// there; the flush is explicit here, whatever the kernel's denormal mode.
+__device__ __forceinline__ float ftz(float x) { return fabsf(x) < FLT_MIN ? 0.f : x; }
+
 __global__ void adam_advance(float* pw) {
-  pw[0] = (pw[0] != 0.f ? pw[0] : kBeta1) * kBeta1;
-  pw[1] = (pw[1] != 0.f ? pw[1] : kBeta2) * kBeta2;
+  const bool started = pw[2] != 0.f;
+  pw[0] = ftz((started ? pw[0] : kBeta1) * kBeta1);
+  pw[1] = ftz((started ? pw[1] : kBeta2) * kBeta2);
+  pw[2] = 1.f;
 }
 
 // touched[x] = val for every id of the batch (rows of a sparse variable the
@@ -870,6 +884,19 @@ extern "C" int hhfm_dfm_train_workspace(int64_t B, int32_t F, int32_t k, int64_t
   return HHFM_OK;
 }
 
+// bytes at the front of the DeepFM workspace that carry state between steps
+// (scalars incl. Adam's β powers, dE, dw, the touched mask); B-independent
+extern "C" int hhfm_dfm_train_state_bytes(int32_t F, int32_t k, int64_t features_M,
+                                          int32_t nlayers, const int32_t* layer_dims,
+                                          size_t* state_bytes) {
+  DfmTrainPlan p;
+  if (!state_bytes || !layer_dims || features_M < 1 ||
+      !dfm_train_plan(1, F, k, features_M, nlayers, layer_dims, p))
+    return HHFM_EINVAL;
+  *state_bytes = (size_t)p.off_WtP[0] * 4;
+  return HHFM_OK;
+}
+
 extern "C" int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F,
                                    float* E, float* w, int64_t features_M, int32_t k,
                                    int32_t nlayers, const int32_t* layer_dims, float* const* W,
@@ -1033,6 +1060,15 @@ extern "C" int hhfm_afm_train_workspace(int64_t B, int32_t F, int32_t k, int32_t
   AfmTrainPlan p;
   if (!ws_bytes || !afm_train_plan(B, F, k, A, features_M, p)) return HHFM_EINVAL;
   *ws_bytes = (size_t)p.total * 4;
+  return HHFM_OK;
+}
+
+// the AFM workspace's persistent prefix (as hhfm_dfm_train_state_bytes)
+extern "C" int hhfm_afm_train_state_bytes(int32_t F, int32_t k, int32_t A, int64_t features_M,
+                                          size_t* state_bytes) {
+  AfmTrainPlan p;
+  if (!state_bytes || !afm_train_plan(1, F, k, A, features_M, p)) return HHFM_EINVAL;
+  *state_bytes = (size_t)p.off_Wt * 4;
   return HHFM_OK;
 }
 

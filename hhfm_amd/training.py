@@ -68,12 +68,14 @@ def _state(model, names, opt):
     return st
 
 
-def _grow(old, nbytes, dev):
-    """A zero-filled train workspace of ``nbytes``; the persistent state at
-    its front (include/hhfm.h: gradients, Adam's β powers) carried over."""
+def _grow(old, nbytes, state_bytes, dev):
+    """A zero-filled train workspace of ``nbytes``; only the persistent prefix
+    of the old one (``state_bytes``: include/hhfm.h hhfm_*_train_state_bytes —
+    gradients, Adam's β powers, the touched mask) carried over, the per-batch
+    scratch after it left zeroed."""
     ws = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
     if old is not None:
-        ws[:old.numel()].copy_(old)
+        ws[:state_bytes].copy_(old[:state_bytes])
     return ws
 
 
@@ -147,7 +149,8 @@ def dfm_partial_fit(model, data) -> float:
     nat = native()
     if st["ws"] is None or st["ws_rows"] < B:
         nbytes = nat.dfm_train_workspace(B, F, k, M, dims)
-        st["ws"] = _grow(st["ws"], nbytes, model.device)
+        st["ws"] = _grow(st["ws"], nbytes, nat.dfm_train_state_bytes(F, k, M, dims),
+                         model.device)
         st["ws_rows"] = B
     ptr = lambda n: W[n].data_ptr()  # noqa: E731
     nat.dfm_train_step(X.data_ptr(), y.data_ptr(), B, F, ptr("feature_embeddings"),
@@ -188,7 +191,7 @@ def afm_partial_fit(model, data) -> float:
     nat = native()
     if st["ws"] is None or st["ws_rows"] < B:
         nbytes = nat.afm_train_workspace(B, F, k, A, M)
-        st["ws"] = _grow(st["ws"], nbytes, model.device)
+        st["ws"] = _grow(st["ws"], nbytes, nat.afm_train_state_bytes(F, k, A, M), model.device)
         st["ws_rows"] = B
     lam = float(model.lamda_attention) if model.lamda_attention > 0 else 0.0
     ptr = lambda n: W[n].data_ptr()  # noqa: E731

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define HHFM_ABI_VERSION 4
+#define HHFM_ABI_VERSION 5
 
 enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 
@@ -357,8 +357,9 @@ int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t F, const vo
  *   2 = MomentumOptimizer(momentum = 0.95)  accum = accum·0.95 + g,
  *       var -= accum·lr; n floats initialised to 0;
  *   3 = AdamOptimizer(β1 0.9, β2 0.999, ε 1e-8)  2n floats (m, then v)
- *       initialised to 0; β1^t, β2^t live in the workspace (zero-filled
- *       once = step 1).
+ *       initialised to 0; β1^t, β2^t and a started flag live in the
+ *       workspace (zero-filled once = step 1; a power that underflows to 0
+ *       stays 0, as TF's does).
  * Variables whose TF gradient is an IndexedSlices (an embedding_lookup with
  * no dense l2 term on the same variable: w of FM; the table of FM / HHFM at
  * λ = 0, of DeepFM and of AFM; w of DeepFM and AFM) follow TF's sparse
@@ -392,11 +393,16 @@ int hhfm_hhfm_train_step(const int32_t* X, const int32_t* Neg, int64_t B, int32_
  * The workspace (hhfm_dfm_train_workspace bytes for batches of at most B rows)
  * must be zero-filled once; the step keeps its gradient regions zeroed.  Its
  * persistent part (gradients, Adam's β powers) leads at offsets independent
- * of B: a workspace grown for a larger batch keeps the state when the old
- * bytes are copied into the front of the new zero-filled one.
+ * of B: a workspace grown for a larger batch keeps the state when that
+ * prefix (hhfm_dfm_train_state_bytes) is copied into the new zero-filled one.
  * Requires k % 4 == 0, L <= 4, F + k + d_{L-1} <= 1024. */
 int hhfm_dfm_train_workspace(int64_t B, int32_t F, int32_t k, int64_t features_M,
                              int32_t nlayers, const int32_t* layer_dims, size_t* ws_bytes);
+/* The size of that persistent prefix (ABI v5): copy exactly these bytes of an
+ * old workspace into a new zero-filled one; everything after it is per-batch
+ * scratch. */
+int hhfm_dfm_train_state_bytes(int32_t F, int32_t k, int64_t features_M, int32_t nlayers,
+                               const int32_t* layer_dims, size_t* state_bytes);
 int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F, float* E,
                         float* w, int64_t features_M, int32_t k, int32_t nlayers,
                         const int32_t* layer_dims, float* const* W, float* const* bias,
@@ -413,11 +419,13 @@ int hhfm_dfm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F
  * pvec, P, sized and initialised as above.  The workspace
  * (hhfm_afm_train_workspace bytes for batches of at most B rows) must be
  * zero-filled once; the step keeps its gradient regions zeroed; grown as for
- * DeepFM (old bytes copied into the front of the new one).
+ * DeepFM (the hhfm_afm_train_state_bytes prefix copied into the new one).
  * Requires 2 <= F <= 16, k and A multiples of 4 and <= 256.  Replaces
  * sess.run((loss, optimizer)) of AFM.partial_fit (AFM.py:205-207). */
 int hhfm_afm_train_workspace(int64_t B, int32_t F, int32_t k, int32_t A,
                              int64_t features_M, size_t* ws_bytes);
+int hhfm_afm_train_state_bytes(int32_t F, int32_t k, int32_t A, int64_t features_M,
+                               size_t* state_bytes);
 int hhfm_afm_train_step(const int32_t* idx, const float* y, int64_t B, int32_t F, float* E,
                         float* w, float* w0, int64_t features_M, int32_t k, int32_t A,
                         float* W, float* b, float* pvec, float* P, float lr,

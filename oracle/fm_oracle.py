@@ -288,12 +288,22 @@ def tf_adagrad(var, grad, acc, lr):
 MOMENTUM, BETA1, BETA2, ADAM_EPS = F32(0.95), F32(0.9), F32(0.999), F32(1e-8)
 
 
+def _ftz(x):
+    """float32 flush-to-zero: TF's CPU thread pools run every op with the
+    FTZ/DAZ flags set (core/lib/core/threadpool.cc, EigenEnvironment::
+    CreateThread: port::ScopedFlushDenormal), so a product below FLT_MIN is 0."""
+    x = F32(x)
+    return F32(0) if abs(x) < np.finfo(F32).tiny else x
+
+
 def adam_powers(step):
     """TF AdamOptimizer's beta1_power / beta2_power at ``step`` (1-based):
-    created at β1, β2 and multiplied by β in float32 after every step (_finish)."""
+    created at β1, β2 and multiplied by β in float32 after every step
+    (_finish), under flush-to-zero: β1^t reaches exactly 0 at t = 829 and
+    stays there (α = lr·√(1−β2^t) from then on)."""
     b1p, b2p = BETA1, BETA2
     for _ in range(step - 1):
-        b1p, b2p = F32(b1p * BETA1), F32(b2p * BETA2)
+        b1p, b2p = _ftz(b1p * BETA1), _ftz(b2p * BETA2)
     return b1p, b2p
 
 

@@ -122,6 +122,58 @@ def test_fm_partial_fit_matches_oracle(opt, lam):
                 _check_slot(m._train_state[n].cpu().numpy(), r, o)
 
 
+def _fm_adam_powers(m):
+    """The FM train workspace's Adam scalars [β1^t, β2^t, started]
+    (train.hip: scal = dE [M·k] + dw [M] floats in)."""
+    M, k = m.weights["feature_embeddings"].shape
+    o = M * k + M + 8
+    return m._train_state["ws"].view(torch.float32)[o:o + 3]
+
+
+def test_fm_adam_past_beta1_power_underflow():
+    """β1^t = 0.9^t underflows to exactly 0 at t = 829 under TF's
+    flush-to-zero and TF keeps using 0 (AdamOptimizer._finish multiplies the
+    power each step), so a zero power must not read as "not started" (the
+    round-4 kernels restarted the powers there: α jumped ~10×).  860 tiny
+    Adam steps: the powers the GPU carries equal adam_powers(t + 1) bit for
+    bit at every checked step, and each step from t = 822 on (across the
+    underflow) is replayed by the oracle from the GPU's own pre-step
+    parameters and slots."""
+    from hhfm_amd.FM import FM
+    rng = np.random.default_rng(5)
+    nu, ni, k = 20, 30, 8
+    X, M = _rows(rng, 64 * 860, nu, ni, (7, 2, 3))
+    Y = rng.integers(0, 2, len(X)).astype(np.float32)[:, None]
+    m = FM(5, M, nu, ni, k, 0.01, 0.1, 1, "AdamOptimizer", 0, 0)
+    m.set_weights(feature_embeddings=rng.normal(0, 0.01, (M, k)).astype(np.float32),
+                  feature_bias=rng.normal(0, 0.01, (M, 1)).astype(np.float32),
+                  bias=np.float32(0.02))
+    names = ["feature_embeddings", "feature_bias", "bias"]
+    crossed = False
+    for t in range(1, 861):
+        Xb, yb = X[(t - 1) * 64:t * 64], Y[(t - 1) * 64:t * 64]
+        if t < 822:
+            m.partial_fit({"X": Xb, "Y": yb})
+            if t % 97 == 0:
+                b1, b2 = orc.adam_powers(t + 1)
+                assert _fm_adam_powers(m).cpu().numpy().tolist() == [b1, b2, 1.0]
+            continue
+        Wg = m.get_weights()
+        cur = [Wg["feature_embeddings"], Wg["feature_bias"][:, 0], np.float32(Wg["bias"])]
+        sl = _slots_of(m, names, "adam", cur)
+        loss = m.partial_fit({"X": Xb, "Y": yb})
+        rl, E1, w1, w01, aE, aw, a0 = orc.fm_train_step(Xb, yb, *cur, *sl, 0.01, 0.1, "adam", t)
+        _, Eg, wg, w0g, *_ = orc.fm_train_step(Xb, yb, *cur, None, None, None, 1.0, 0.1, "sgd")
+        assert np.isclose(loss, rl, rtol=1e-5)
+        Wn = m.get_weights()
+        _check_var(Wn["feature_embeddings"], E1, cur[0], "adam", cur[0] - Eg)
+        _check_var(Wn["feature_bias"][:, 0], w1, cur[1], "adam", cur[1] - wg)
+        b1, b2 = orc.adam_powers(t + 1)
+        assert _fm_adam_powers(m).cpu().numpy().tolist() == [b1, b2, 1.0]
+        crossed |= b1 == 0.0
+    assert crossed
+
+
 HHFM_CASES = [("frappe", "AdagradOptimizer", 0.01), ("jiaju", "AdagradOptimizer", 0.01),
               ("frappe", "MomentumOptimizer", 0.0), ("jiaju", "MomentumOptimizer", 0.01),
               ("frappe", "AdamOptimizer", 0.0), ("jiaju", "AdamOptimizer", 0.01),

@@ -215,3 +215,20 @@ def test_tf_adam_dense_and_sparse():
     assert E1[1, 0] == E[1, 0] and E1[2, 0] == E[2, 0]     # m = 0 there: no move
     E2, t2 = orc.tf_apply("adam", E1, np.zeros_like(gs), t1, 0.1, 2, rows=np.array([1]))
     assert np.allclose(t2[:4], 0.9 * t1[:4]) and E2[0, 0] < E1[0, 0] and E2[3, 0] > E1[3, 0]
+
+
+def test_tf_adam_powers_flush_to_zero():
+    """TF multiplies beta1_power by β1 on FTZ/DAZ threads: the power falls
+    from the smallest normal product straight to 0 at t = 829 and stays 0
+    (never a denormal); α = lr·√(1 − β2^t) from then on."""
+    b1_828, _ = orc.adam_powers(828)
+    assert b1_828 >= np.finfo(np.float32).tiny
+    for t in (829, 830, 1000, 2000):
+        b1p, b2p = orc.adam_powers(t)
+        assert b1p == 0.0 and 0.0 < b2p < 1.0
+    v = np.float32([1.0, -2.0])
+    g = np.float32([0.3, -0.02])
+    slot = np.float32([0.01, -0.001, 1e-4, 1e-6])
+    v1, s1 = orc.tf_apply("adam", v, g, slot, 0.01, step=900)
+    alpha = np.float32(0.01 * np.sqrt(np.float32(1) - orc.adam_powers(900)[1], dtype=np.float32))
+    assert np.allclose(v - v1, alpha * s1[:2] / (np.sqrt(s1[2:]) + 1e-8), rtol=1e-5)
