@@ -99,7 +99,7 @@ struct BoolC {
 
 // the 256-row kernel (dfm_wide.hip) at an instantiated shape; false: not
 // instantiated (the caller runs dfm_fused)
-bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st);
+bool dfm_wide_launch(const FusedDfmArgs& a, int TM, int32_t plan, hipStream_t st);
 // base[m] = (Σ_f w·Wp + FM part) + bp into a.fm_out from the pair table
 // C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip; built once per call into a.scratch); false
 // (nothing launched) when it does not fit a.scratch, the rows are too few to

@@ -1711,7 +1711,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
     return true;
   }
   // the ITEM plan at an instantiated shape: 256 rows per workgroup (dfm_wide.hip)
-  if (pj && tbf && a.Fd == 1 && L == 3 && !(plan & HHFM_PLAN_NARROW) && dfm_wide_launch(a, TM, st))
+  if (pj && tbf && a.Fd == 1 && L == 3 && !(plan & HHFM_PLAN_NARROW) &&
+      dfm_wide_launch(a, TM, plan, st))
     return true;
   const dim3 grid((unsigned)((B + kFusedRows - 1) / kFusedRows));
   const int nS = a.Fd * (k / 16), nc0 = (nS + 3) / 4, NC = (TM + 1) / 2;

@@ -52,7 +52,14 @@ namespace hhfm {
 // per SIMD (C5 bf16 10.0-10.3 ms, bit-identical), against 3 x 4 = 192 rows at
 // one wave per SIMD (12.9-13.0 ms; profiles/r04_k3w_two_waves_ab.txt): the
 // second wave's MFMAs cover the first's DMA issue, epilogue and barrier waits,
-// and each weight byte streamed feeds 256 rows instead of 192
+// and each weight byte streamed feeds 256 rows instead of 192.  The template
+// admits RT in 1..3 at 4 waves and RT <= 2 at 8 (at most 16 row tiles); the
+// plan bits HHFM_PLAN_WIDE_* run the alternates at the test shape, and every
+// admitted shape was measured bit-identical to the default at C5 as well
+// (profiles/r05_wide_shapes.txt).  (The wrong results of round-4 scratch logs
+// gpurun_out/wide_r{1,2}w4.log came from a working tree before commit
+// 5f4698f, which sized the per-wave vmcnt wait from the DMA units each wave
+// issues; the committed template was never wrong at those shapes.)
 #ifndef HHFM_WIDE_RT
 #define HHFM_WIDE_RT 2
 #endif
@@ -169,6 +176,8 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
   // PAIRS: a.fmbase[m] = (Σ_f w·Wp + FM part) + bp from the pair table
   // (dfm_fm_pairs), so no table rows are staged and no FM part runs here
   static_assert(NF >= 1 && NF < kFusedMaxF, "wide DeepFM kernel: fields");
+  static_assert((NWV == 4 || NWV == 8) && RT >= 1 && RT <= 3 && RT * NWV <= 16,
+                "wide DeepFM kernel: 1-3 row tiles at 4 waves, 1-2 at 8");
   constexpr int F = NF + 1;
   constexpr int NR = TM * 32;
   constexpr int NCH = 3 * TM;                          // passes: (layer, 32 units)
@@ -607,32 +616,41 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
   else body(BoolC<false>{});
 }
 
-bool dfm_wide_launch(const FusedDfmArgs& a, int TM, hipStream_t st) {
+template <int T, int A, int N, int RT, int NWV>
+static void wide_launch_shape(const FusedDfmArgs& a, hipStream_t st) {
+  constexpr int kRowsWG = NWV * 16 * RT;
+  const dim3 grid((unsigned)((a.B + kRowsWG - 1) / kRowsWG));
+  const int64_t units = ((int64_t)T * A * 2 + 2 * (int64_t)T * T * 2) * 64;
+  const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+  hipLaunchKernelGGL(dfm_pack_weights_w, dim3(pblocks), dim3(256), 0, st, a, T, A,
+                     const_cast<uint4*>(a.packed));
+  if (dfm_fm_pairs(a, true, st)) {
+    FusedDfmArgs b = a;
+    b.fmbase = a.fm_out;
+    hipLaunchKernelGGL((dfm_fused_w<T, A, N, true, RT, NWV>), grid, dim3(NWV * 64), 0, st, b);
+  } else {
+    hipLaunchKernelGGL((dfm_fused_w<T, A, N, false, RT, NWV>), grid, dim3(NWV * 64), 0, st, a);
+  }
+}
+
+bool dfm_wide_launch(const FusedDfmArgs& a, int TM, int32_t plan, hipStream_t st) {
   bool ok = a.L == 3 && a.Fd == 1 && a.k % 32 == 0;
   for (int i = 0; i < 3; ++i) ok = ok && (a.dims[i] + 31) / 32 == TM;
   if (!ok) return false;
   const int S0 = a.k / 32;
   constexpr int kRT = HHFM_WIDE_RT, kNWV = HHFM_WIDE_NWV;
-  constexpr int kRowsWG = kNWV * 16 * kRT;
-  const dim3 grid((unsigned)((a.B + kRowsWG - 1) / kRowsWG));
-  const int64_t units = ((int64_t)TM * S0 * 2 + 2 * (int64_t)TM * TM * 2) * 64;
-  const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
-  uint4* packed = const_cast<uint4*>(a.packed);
-#define HHFM_WIDE(T, A, N)                                                                 \
-  if (TM == T && S0 == A && a.F == N + 1) {                                                \
-    hipLaunchKernelGGL(dfm_pack_weights_w, dim3(pblocks), dim3(256), 0, st, a, T, A, packed); \
-    if (dfm_fm_pairs(a, true, st)) {                                                       \
-      FusedDfmArgs b = a;                                                                  \
-      b.fmbase = a.fm_out;                                                                 \
-      hipLaunchKernelGGL((dfm_fused_w<T, A, N, true, kRT, kNWV>), grid, dim3(kNWV * 64), 0, st, b);         \
-    } else {                                                                               \
-      hipLaunchKernelGGL((dfm_fused_w<T, A, N, false, kRT, kNWV>), grid, dim3(kNWV * 64), 0, st, a);        \
-    }                                                                                      \
-    return true;                                                                           \
+  const int shape = plan & HHFM_PLAN_WIDE_MASK;
+  if (TM == 13 && S0 == 8 && a.F == 5) {   // C5: F = 5, k = 256, 3 x 400
+    wide_launch_shape<13, 8, 4, kRT, kNWV>(a, st);
+    return true;
   }
-  HHFM_WIDE(13, 8, 4)   // C5: F = 5, k = 256, 3 x 400
-  HHFM_WIDE(5, 2, 4)    // tests: F = 5, k = 64, 3 x 150
-#undef HHFM_WIDE
+  if (TM == 5 && S0 == 2 && a.F == 5) {    // tests: F = 5, k = 64, 3 x 150
+    if (shape == HHFM_PLAN_WIDE_3X4) wide_launch_shape<5, 2, 4, 3, 4>(a, st);
+    else if (shape == HHFM_PLAN_WIDE_2X4) wide_launch_shape<5, 2, 4, 2, 4>(a, st);
+    else if (shape == HHFM_PLAN_WIDE_1X4) wide_launch_shape<5, 2, 4, 1, 4>(a, st);
+    else wide_launch_shape<5, 2, 4, kRT, kNWV>(a, st);
+    return true;
+  }
   return false;
 }
 

@@ -177,6 +177,27 @@ PYBIND11_MODULE(_hhfm, m) {
           check(rc, "hhfm_topk_walk");
         });
 
+  m.def("sample_negative_workspace", [](int64_t B, int num) {
+    size_t n = 0;
+    check(hhfm_sample_negative_workspace(B, num, &n), "hhfm_sample_negative_workspace");
+    return n;
+  });
+
+  m.def("sample_negative",
+        [](uptr state, int64_t lo, int64_t hi, uptr rows, int64_t B, int ncols, int item_col,
+           int num, uptr keys, int64_t nkeys, uptr codes, int64_t ncodes, uptr samples, uptr ws,
+           size_t ws_bytes, uptr stream) {
+          int rc;
+          {
+            py::gil_scoped_release nogil;
+            rc = hhfm_sample_negative(P<uint32_t>(state), lo, hi, P<const int32_t>(rows), B,
+                                      ncols, item_col, num, P<const int32_t>(keys), nkeys,
+                                      P<const int64_t>(codes), ncodes, P<int64_t>(samples),
+                                      P<void>(ws), ws_bytes, P<void>(stream));
+          }
+          check(rc, "hhfm_sample_negative");
+        });
+
   m.def("libfm_encode",
         [](py::bytes buf, int ncols, int64_t max_rows, uptr labels, uptr ids, uptr distinct) {
           std::string_view v = buf;

@@ -21,13 +21,15 @@ The model is duck-typed: ``model.score_rows(X) -> float32 [B,1]`` (replaces
 ``model.topk(A, tp) -> int [B,tp]`` item offsets.
 
 With a model on the GPU (``model.device`` a cuda device) the per-element
-work runs on the device: the rejection test of
-``sample_negative`` and evaluate_TopK's target test through
-``hhfm_pf_contains`` (positive_feedback as sorted key / (key, item) code
-arrays, ``DevicePairSet``), the metric walk through ``hhfm_topk_walk``.
-The random draws stay on the host (numpy's stream) and the walk's ranks are
-turned into the reference's float64 values on the host, so the results are
-identical to the host path (tests/test_gpu_harness.py).
+work runs on the device: ``sample_negative`` as a
+whole through ``hhfm_sample_negative`` (numpy's MT19937 stream generated on
+the device, masked bounded draws, membership and the row-major re-draws;
+the host's RandomState resumes from the state it returns),
+evaluate_TopK's target test through ``hhfm_pf_contains`` (positive_feedback
+as sorted key / (key, item) code arrays, ``DevicePairSet``) and the metric
+walk through ``hhfm_topk_walk``.  The walk's ranks are turned into the
+reference's float64 values on the host, so the results are identical to
+the host path (tests/test_gpu_harness.py).
 """
 from __future__ import annotations
 
@@ -160,23 +162,18 @@ class Train(object):
         return d[2]
 
     def sample_negative(self, data, num=10):
-        """FM.py:284-294 with the same np.random stream."""
+        """FM.py:284-294 with the same np.random stream.  With a GPU model the
+        whole call — block draw, membership, re-draws — runs on the device
+        on numpy's own MT19937 stream (hhfm_sample_negative), and the global
+        RandomState continues exactly where the reference's would."""
         lo, hi = self.n_user, self.n_user + self.n_item
+        dev = self._device()
+        if dev is not None and len(data) > 0:
+            return self._device_sample_negative(dev, np.asarray(data), num, lo, hi)
         samples = np.random.randint(lo, hi, size=(len(data), num))
         if len(data) == 0:
             return samples
         pf = self.data.positive_feedback
-        dev = self._device()
-        if dev is not None:
-            data = np.asarray(data)
-            bad = self._device_pairs(dev, data.shape[1] - 1).contains(data, samples)
-            kcols = [c for c in range(data.shape[1]) if c != 1]
-            for i, j in np.argwhere(bad):      # row-major, like the nested loop
-                key = tuple(data[i, kcols].tolist())
-                neg = samples[i, j]
-                while neg in pf[key]:
-                    samples[i, j] = neg = np.random.randint(lo, hi)
-            return samples
         keys = row_keys(data)
         bad = self._pair_index().contains(keys, samples)
         for i, j in np.argwhere(bad):      # row-major, like the nested loop
@@ -185,6 +182,45 @@ class Train(object):
             while neg in pf[key]:
                 samples[i, j] = neg = np.random.randint(lo, hi)
         return samples
+
+    def _device_sample_negative(self, dev, data, num, lo, hi):
+        """hhfm_sample_negative: the legacy RandomState's (key, pos) in, the
+        samples and the state after the call's last word out."""
+        import torch
+        from . import ops
+        from ._native import native
+        st = np.random.get_state()
+        if st[0] != "MT19937":
+            raise ValueError(f"np.random state {st[0]!r}: the device sampler follows MT19937")
+        state = np.empty(625, np.uint32)
+        state[:624] = st[1]
+        state[624] = st[2]
+        B, ncols = data.shape
+        pairs = self._device_pairs(dev, ncols - 1)
+        nat = native()
+        nbytes = nat.sample_negative_workspace(B, num)
+        cache = getattr(self, "_sampler_bufs", None)
+        if cache is None or cache["dev"] != dev or cache["ws"].numel() < nbytes or \
+                cache["host"].numel() < B * num:
+            cache = self._sampler_bufs = {
+                "dev": dev, "ws": torch.empty(nbytes, dtype=torch.uint8, device=dev),
+                "host": torch.empty(B * num, dtype=torch.int64, pin_memory=True),
+                "state": torch.empty(625, dtype=torch.int32, pin_memory=True)}
+        sd = torch.from_numpy(state.view(np.int32)).to(dev)
+        rows = torch.from_numpy(np.ascontiguousarray(data, dtype=np.int32)).to(dev)
+        out = torch.empty(B * num, dtype=torch.int64, device=dev)
+        nat.sample_negative(sd.data_ptr(), lo, hi, rows.data_ptr(), B, ncols, 1, num,
+                            pairs.keys.data_ptr() if pairs.n else 0, pairs.n,
+                            pairs.codes.data_ptr() if pairs.n else 0, pairs.codes.numel(),
+                            out.data_ptr(), cache["ws"].data_ptr(), cache["ws"].numel(),
+                            ops._stream(dev))
+        host, hstate = cache["host"][:B * num], cache["state"]
+        host.copy_(out, non_blocking=True)
+        hstate.copy_(sd, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        new = hstate.numpy().view(np.uint32)
+        np.random.set_state((st[0], new[:624].copy(), int(new[624]), st[3], st[4]))
+        return host.numpy().reshape(B, num).copy()
 
     # -- H4 -----------------------------------------------------------------
     def evaluate_AUC(self, data1):

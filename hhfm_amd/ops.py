@@ -30,6 +30,9 @@ PLAN_UNGROUPED = 1 << 7
 PLAN_NARROW = 1 << 8
 PLAN_PER_FIELD = 1 << 9
 PLAN_ONE_WAVE = 1 << 10
+PLAN_WIDE_3X4 = 1 << 11   # DeepFM 256-row kernel shapes (test shape only)
+PLAN_WIDE_2X4 = 2 << 11
+PLAN_WIDE_1X4 = 3 << 11
 
 
 def _dtype_code(t: torch.Tensor) -> int:

@@ -61,7 +61,15 @@ enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 #define HHFM_PLAN_PER_FIELD (1 << 9)  /* AFM catalog: pair product split per query field
                                          (afm_cat_fused), not the folded weights */
 #define HHFM_PLAN_ONE_WAVE (1 << 10)  /* dense top-K: one wave per query at every size */
-#define HHFM_PLAN_ALL ((1 << 11) - 1)
+/* DeepFM bf16 ITEM plan, 256-row kernel: its workgroup shape (16-row tiles per
+ * wave x waves) — 0 the default 2 x 8; these alternates are instantiated for
+ * the k = 64, 3 x 150 test shape only (ABI v5), so every shape the kernel
+ * template admits runs in the parity tests (bit-identical by construction) */
+#define HHFM_PLAN_WIDE_3X4 (1 << 11)
+#define HHFM_PLAN_WIDE_2X4 (2 << 11)
+#define HHFM_PLAN_WIDE_1X4 (3 << 11)
+#define HHFM_PLAN_WIDE_MASK (3 << 11)
+#define HHFM_PLAN_ALL ((1 << 13) - 1)
 
 /* catalog scoring modes */
 enum hhfm_catalog_mode {
@@ -469,6 +477,31 @@ int hhfm_pf_contains(const int32_t* keys, int64_t nkeys, int32_t key_cols,
                      const int32_t* cand, int32_t num, uint8_t* out, void* stream);
 int hhfm_topk_walk(const int32_t* pred, int64_t B, int32_t P, const int32_t* target,
                    const uint8_t* positive, int32_t TopK, int32_t* outcome, void* stream);
+
+/* hhfm_sample_negative (ABI v5) — all of Train.sample_negative
+ * (FM.py:284-294) on the device, on numpy's own random stream:
+ *   samples = np.random.randint(lo, hi, size=(B, num)), then in row-major
+ *   order each sample that is in positive_feedback[key of its row] re-drawn
+ *   with np.random.randint(lo, hi) until it is not.
+ * mt_state: device uint32 [625] = the legacy RandomState's MT19937 key[624]
+ * followed by pos (np.random.get_state()[1:3]); on return it holds the state
+ * after the last word the call read, for np.random.set_state — the samples
+ * and the state equal the reference's bit for bit (numpy's masked bounded
+ * draw: 32-bit outputs AND the smallest covering mask, rejected while > hi -
+ * 1 - lo).  rows int32 [B][ncols] (key = every column but item_col), keys /
+ * codes as for hhfm_pf_contains; samples: device int64 [B][num].  Requires
+ * 0 <= lo < hi <= 2^31, B·num < 2^30.  A row whose positives cover all of
+ * [lo, hi) (where the reference loops forever) returns HHFM_EINVAL.  Unlike
+ * the other entry points this call synchronises `stream` (a few small
+ * device-to-host reads steer the generation rounds); the workspace is
+ * hhfm_sample_negative_workspace(B, num) bytes, no initialisation needed.
+ * Replaces FM.py:284-294 (and OurModel7.py, AFM.py, DFM.py's copies). */
+int hhfm_sample_negative_workspace(int64_t B, int32_t num, size_t* ws_bytes);
+int hhfm_sample_negative(uint32_t* mt_state, int64_t lo, int64_t hi, const int32_t* rows,
+                         int64_t B, int32_t ncols, int32_t item_col, int32_t num,
+                         const int32_t* keys, int64_t nkeys, const int64_t* codes,
+                         int64_t ncodes, int64_t* samples, void* workspace, size_t ws_bytes,
+                         void* stream);
 
 /* ------------------------------------------------------------------------
  * L1 — the libfm loader's per-cell work (NewLoadData.py:16-58), HOST code:

@@ -460,3 +460,10 @@ def test_dfm_wide_item(k, layers, B, grouped):
     if B >= 16 * M:
         rows_fm = run(xd, ops.PLAN_ROW_FM)
         assert np.all(np.abs(rows_fm - ref) <= 5e-3 * mag), np.max(np.abs(rows_fm - ref) / mag)
+    if k == 64:
+        # every workgroup shape the kernel template admits (16-row tiles per
+        # wave x waves: 3x4, 2x4, 1x4 besides the default 2x8): bit-identical
+        for shape in (ops.PLAN_WIDE_3X4, ops.PLAN_WIDE_2X4, ops.PLAN_WIDE_1X4):
+            alt = run(xd, shape)
+            assert np.all(np.abs(alt - ref) <= 5e-3 * mag), (shape, np.max(np.abs(alt - ref) / mag))
+            assert np.array_equal(alt, got), shape

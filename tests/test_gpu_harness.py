@@ -131,3 +131,93 @@ def test_sample_negative_device_equals_host_at_frappe_shape(tmp_path):
     np.random.seed(99)
     host.sample_negative(X, 50)
     assert np.random.randint(1 << 30) == nxt_dev
+
+
+def _state_eq(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3:] == b[3:]
+
+
+def _both(t_host, t_dev, X, num, prime):
+    """host and device sample_negative from the same RandomState: samples
+    and the state after the call (np.random.get_state) must be equal."""
+    prime()
+    s0 = np.random.get_state()
+    a = t_host.sample_negative(X, num)
+    sa = np.random.get_state()
+    np.random.set_state(s0)
+    b = t_dev.sample_negative(X, num)
+    sb = np.random.get_state()
+    assert a.dtype == b.dtype and a.shape == b.shape
+    assert np.array_equal(a, b), int((a != b).sum())
+    assert _state_eq(sa, sb), (sa[2], sb[2])
+    return a
+
+
+def test_sample_negative_on_device_frappe_shape_state(tmp_path):
+    """The whole sampler on the device (hhfm_sample_negative: MT19937 words,
+    masked bounded draws, membership, row-major re-draws) at the row-table
+    shape — every Frappe-shape train row, 50 negatives (evaluate_AUC's draw):
+    the samples AND numpy's generator state afterwards equal the host
+    harness's (the reference's stream), from a fresh seed (pos 624), from
+    mid-block positions, and from pos = 624 after a full block."""
+    import bench
+    from hhfm_amd.NewLoadData import LoadData
+    np.random.seed(2016)
+    d = LoadData(bench.frappe_shape_dataset(str(tmp_path)), "frappe_shape")
+    X = np.asarray(d.Train_data.values[:, 1:], dtype=np.int64)
+    host = harness.Train(data=d, model=None)
+    devt = harness.Train(data=d, model=DeviceOracleModel(None, None, d.n_user, d.n_item))
+    _both(host, devt, X, 50, lambda: np.random.seed(99))
+    _both(host, devt, X[:1000], 2, lambda: (np.random.seed(5), np.random.randint(0, 7, 333)))
+    _both(host, devt, X[:777], 10,
+          lambda: (np.random.seed(6), np.random.randint(0, 1 << 32, 624, dtype=np.uint64)))
+    # a second call continues the stream like the reference's
+    np.random.seed(3)
+    a1, a2 = host.sample_negative(X[:5000], 10), host.sample_negative(X[5000:9000], 50)
+    np.random.seed(3)
+    b1, b2 = devt.sample_negative(X[:5000], 10), devt.sample_negative(X[5000:9000], 50)
+    assert np.array_equal(a1, b1) and np.array_equal(a2, b2)
+
+
+class _PF:
+    def __init__(self, pf, n_user, n_item):
+        self.positive_feedback, self.n_user, self.n_item = pf, n_user, n_item
+
+
+@pytest.mark.parametrize("n_item,cover", [(5, 0.8), (2, 0.5), (64, 0.9), (65, 0.5),
+                                          (1000, 0.97), (1, 0.0)])
+def test_sample_negative_on_device_heavy_rejection(n_item, cover):
+    """Keys whose positives cover most of the catalog force long re-draw
+    chains (several rounds of 256 entries, values running out, generation
+    rounds that slide the MT window); catalogs of 2^k and 2^k + 1 items set
+    the mask's rejection rate to 0 and ~1/2; one item draws nothing
+    (randint(lo, lo + 1)).  Device == host harness, samples and state."""
+    rng = np.random.default_rng(n_item)
+    n_user, ncols = 40, 4
+    keys = [tuple(int(v) for v in rng.integers(0, 50, ncols - 1)) for _ in range(60)]
+    pf = {}
+    for k in keys:
+        n_pos = min(int(cover * n_item), n_item - 1)
+        pf[k] = set(int(n_user + i) for i in rng.choice(n_item, n_pos, replace=False))
+    rows = []
+    for _ in range(3000):
+        k = keys[rng.integers(0, len(keys))] if rng.random() < 0.9 else (99, 99, 99)
+        rows.append([k[0], n_user, k[1], k[2]])
+    X = np.asarray(rows, dtype=np.int64)
+    data = _PF(pf, n_user, n_item)
+    host = harness.Train(data=data, model=None)
+    devt = harness.Train(data=data, model=DeviceOracleModel(None, None, n_user, n_item))
+    for seed, num in ((1, 10), (2, 1), (3, 50)):
+        _both(host, devt, X, num, lambda: np.random.seed(seed))
+
+
+def test_sample_negative_on_device_refuses_a_hang():
+    """A key whose positives are the whole catalog makes the reference loop
+    forever (FM.py:291-293); the device sampler reports it instead."""
+    n_user, n_item = 10, 4
+    pf = {(1, 2, 3): set(range(n_user, n_user + n_item))}
+    X = np.asarray([[1, n_user, 2, 3]] * 5, dtype=np.int64)
+    devt = harness.Train(data=_PF(pf, n_user, n_item),
+                         model=DeviceOracleModel(None, None, n_user, n_item))
+    with pytest.raises(ValueError):
+        devt.sample_negative(X, 3)
