@@ -17,9 +17,27 @@
 // AFM.py:223,230) is kept.
 #include <cstdlib>
 
+#include <atomic>
+
 #include "gemm_mfma.h"
 
 namespace hhfm {
+
+// CUs of the device that owns `st` (the stream's device, not the calling
+// thread's current one), cached per device: the persistent grids ask per call
+static int stream_cu_count(hipStream_t st) {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= 64) return 256;
+  int c = cache[dev].load(std::memory_order_relaxed);
+  if (c <= 0) {
+    c = 256;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    cache[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
+}
 
 static size_t a256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -1475,9 +1493,7 @@ extern "C" int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t 
         }
         if (wl <= 160 * 1024) {
           // one block per CU walks an equal share of the query-major tiles
-          int dev = 0, cus = 256;
-          if (hipGetDevice(&dev) == hipSuccess)
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+          const int cus = stream_cu_count(st);
           const int64_t T = nq * (int64_t)ntile;
           const dim3 wgrid((unsigned)(T < cus ? T : cus));
 #define HHFM_AFM_CAT_W_L(N, TB, KS)                                                              \

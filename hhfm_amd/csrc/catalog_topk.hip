@@ -862,6 +862,12 @@ __global__ __launch_bounds__(256) void topk_merge_kernel(
   }
 }
 
+}  // namespace hhfm
+
+#include "catalog_fused.h"
+
+namespace hhfm {
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -871,6 +877,7 @@ struct Plan {
   bool dense;            // small catalog: score matrix + dense top-K
   int64_t ldsc;
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
+  int fS, fT;            // fused small-catalog kernel: workgroups per 32 queries, tiles per wave
   int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
       off_seed_i, total;
@@ -933,6 +940,22 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
     off += align256((size_t)B * nsplit * K * sizeof(int32_t));
   } else {
     p.off_pi = off;
+  }
+  // the fused small-catalog kernel (catalog_fused.h): S_f workgroups per
+  // 32 queries, each kFusedWaves waves x kFusedTiles tiles; S_f > 1 merges
+  // lists of K from off_ps
+  {
+    constexpr int kTilesWG = kFusedWaves * kFusedTiles;
+    p.fS = (ntiles + kTilesWG - 1) / kTilesWG;
+    // (8 tiles per wave, half the workgroups, spilled ~150 registers: not kept)
+    p.fT = kFusedTiles;
+    const int fS4 = p.fS;
+    if (p.dense && fS4 > 1 && nsplit < fS4) {
+      off = p.off_ps;
+      off += align256((size_t)B * fS4 * K * sizeof(float));
+      p.off_pi = off;
+      off += align256((size_t)B * fS4 * K * sizeof(int32_t));
+    }
   }
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
@@ -1051,6 +1074,55 @@ static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const fl
                        ldsc, 0, 0, gthr);
 }
 
+template <bool BF16, int KT, bool FM, int T>
+static void launch_fused_t(int64_t B, int nqb, int S, const int32_t* qidx, int ncols, int mode,
+                         int ucol, int c0, int c1, int t0, int t1, const char* E, int64_t M,
+                         int64_t irb, int32_t N, const float* w, int K, float* os, int32_t* oi,
+                         int64_t sb, int64_t ss, int32_t gbase, int32_t plan, hipStream_t st) {
+  constexpr bool kCanSplit = BF16 || KT >= 2;
+  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
+    hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, kCanSplit, T>), dim3(nqb * S),
+                       dim3(kFusedWaves * 64), 0, st,
+                       qidx, B, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, S, os, oi,
+                       sb, ss, gbase);
+  else
+    hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, false, T>), dim3(nqb * S),
+                       dim3(kFusedWaves * 64), 0, st,
+                       qidx, B, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, S, os, oi,
+                       sb, ss, gbase);
+}
+
+template <bool BF16, int KT, bool FM>
+static void launch_fused(int T, int64_t B, int nqb, int S, const int32_t* qidx, int ncols,
+                         int mode, int ucol, int c0, int c1, int t0, int t1, const char* E,
+                         int64_t M, int64_t irb, int32_t N, const float* w, int K, float* os,
+                         int32_t* oi, int64_t sb, int64_t ss, int32_t gbase, int32_t plan,
+                         hipStream_t st) {
+  (void)T;
+  launch_fused_t<BF16, KT, FM, kFusedTiles>(B, nqb, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E,
+                                            M, irb, N, w, K, os, oi, sb, ss, gbase, plan, st);
+}
+
+template <bool BF16, bool FM>
+static bool dispatch_fused(int KT, int T, int64_t B, int nqb, int S, const int32_t* qidx, int ncols,
+                           int mode, int ucol, int c0, int c1, int t0, int t1, const char* E,
+                           int64_t M, int64_t irb, int32_t N, const float* w, int K, float* os,
+                           int32_t* oi, int64_t sb, int64_t ss, int32_t gbase, int32_t plan,
+                           hipStream_t st) {
+#define HHFM_FUSED(KT_) \
+  launch_fused<BF16, KT_, FM>(T, B, nqb, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, \
+                              w, K, os, oi, sb, ss, gbase, plan, st)
+  switch (KT) {
+    case 1: HHFM_FUSED(1); break;
+    case 2: HHFM_FUSED(2); break;
+    case 4: HHFM_FUSED(4); break;
+    case 8: HHFM_FUSED(8); break;
+    default: return false;
+  }
+#undef HHFM_FUSED
+  return true;
+}
+
 template <bool BF16, bool FM>
 static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H,
                            const float* cst, const char* E, int64_t irb, const float* w,
@@ -1158,6 +1230,37 @@ extern "C" int hhfm_catalog_topk_ex(
     const int rc = launch_check_query_ids(qidx, B, ncols, user_col, ctx_begin, ctx_end,
                                           time_begin, time_end, features_M, status, st);
     if (rc != HHFM_OK) return rc;
+  }
+
+  // small catalogs: scores and top-K in one kernel (catalog_fused.h) for
+  // >= 1,024 queries; fewer run latency-bound on few CUs, where the score
+  // matrix path measured faster (300 queries: 22.4 vs 24.8 us of kernel
+  // time; 3,000: 46.1 vs 44.0, profiles/r05_c3_paths.txt).  HHFM_PLAN_STORE
+  // forces the matrix path, HHFM_PLAN_FUSED the fused kernel at any size.
+  const bool fused_size = B >= 1024 || (plan & HHFM_PLAN_FUSED);
+  if (p.dense && fused_size && K <= 32 && KT <= 8 &&
+      ctx_end - ctx_begin <= kFusedMaxCtx && time_end - time_begin <= kFusedMaxCtx &&
+      !(plan & (HHFM_PLAN_GEMM | HHFM_PLAN_STORE))) {
+    const bool fmm = mode == HHFM_MODE_FM;
+    const float* wv = (fmm && w) ? w : nullptr;
+    float* os = p.fS > 1 ? reinterpret_cast<float*>(ws + p.off_ps) : top_score;
+    int32_t* oi = p.fS > 1 ? reinterpret_cast<int32_t*>(ws + p.off_pi) : top_idx;
+    const int64_t sb = (int64_t)p.fS * K, ss = p.fS > 1 ? K : 0;
+    const int32_t gb = global_item_base;   // order-preserving shift
+    const int nqb32 = (int)((B + kQPerWave - 1) / kQPerWave);
+#define HHFM_FARGS KT, p.fT, B, nqb32, p.fS, qidx, ncols, mode, user_col, ctx_begin, ctx_end, \
+    time_begin, time_end, Eb, features_M, (int64_t)item_row_begin, item_count, wv, K, os, oi, \
+    sb, ss, gb, plan, st
+    const bool ok = bf16 ? (fmm ? dispatch_fused<true, true>(HHFM_FARGS)
+                                : dispatch_fused<true, false>(HHFM_FARGS))
+                         : (fmm ? dispatch_fused<false, true>(HHFM_FARGS)
+                                : dispatch_fused<false, false>(HHFM_FARGS));
+#undef HHFM_FARGS
+    if (ok) {
+      if (p.fS > 1)
+        launch_merge(os, oi, p.fS, B, K, /*stride_r=*/K, /*stride_b=*/sb, top_score, top_idx, st);
+      return (int)hipGetLastError();
+    }
   }
 
   {

@@ -33,6 +33,8 @@ PLAN_ONE_WAVE = 1 << 10
 PLAN_WIDE_3X4 = 1 << 11   # DeepFM 256-row kernel shapes (test shape only)
 PLAN_WIDE_2X4 = 2 << 11
 PLAN_WIDE_1X4 = 3 << 11
+PLAN_STORE = 1 << 13      # small catalog: score matrix + dense top-K (not the fused kernel)
+PLAN_FUSED = 1 << 14      # small catalog: the fused score-and-select kernel at any query count
 
 
 def _dtype_code(t: torch.Tensor) -> int:

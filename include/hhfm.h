@@ -69,7 +69,12 @@ enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 #define HHFM_PLAN_WIDE_2X4 (2 << 11)
 #define HHFM_PLAN_WIDE_1X4 (3 << 11)
 #define HHFM_PLAN_WIDE_MASK (3 << 11)
-#define HHFM_PLAN_ALL ((1 << 13) - 1)
+#define HHFM_PLAN_STORE (1 << 13)     /* small catalog: the score matrix materialised by the
+                                         catalog kernel + dense top-K, not the fused
+                                         score-and-select kernel (ABI v5) */
+#define HHFM_PLAN_FUSED (1 << 14)     /* small catalog: the fused kernel at any query count
+                                         (default: from 1,024 queries) (ABI v5) */
+#define HHFM_PLAN_ALL ((1 << 15) - 1)
 
 /* catalog scoring modes */
 enum hhfm_catalog_mode {

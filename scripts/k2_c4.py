@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.append(ROOT)   # a PYTHONPATH package copy (scripts/k2_libs.sh) wins
 from hhfm_amd import ops  # noqa: E402
 
 

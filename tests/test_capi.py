@@ -81,12 +81,12 @@ def test_plan_and_flag_bits_validated_without_device():
     assert lib.hhfm_fm_score_rows_ex(None, 10, 5, None, 10, 64, 0, None, 0.0, None, 1 << 4,
                                      None, None) == -1
     lib.hhfm_topk_dense_ex.argtypes = [vp, i64, i32, i64, i32, i32, vp, vp, i32, vp]
-    assert lib.hhfm_topk_dense_ex(None, 4, 100, 100, 5, 0, None, None, 1 << 13, None) == -1
+    assert lib.hhfm_topk_dense_ex(None, 4, 100, 100, 5, 0, None, None, 1 << 15, None) == -1
     assert lib.hhfm_topk_dense_ex(None, 0, 100, 100, 5, 0, None, None, 1 << 10, None) == 0
     lib.hhfm_afm_catalog_topk_workspace_ex.argtypes = [i64, i32, i32, i32, i32, i64, i32,
                                                        ctypes.POINTER(ctypes.c_size_t)]
     ws = ctypes.c_size_t(0)
-    assert lib.hhfm_afm_catalog_topk_workspace_ex(300, 5, 64, 64, 4082, 1 << 17, 1 << 13,
+    assert lib.hhfm_afm_catalog_topk_workspace_ex(300, 5, 64, 64, 4082, 1 << 17, 1 << 15,
                                                   ctypes.byref(ws)) == -1
     fused, gemm = ctypes.c_size_t(0), ctypes.c_size_t(0)
     assert lib.hhfm_afm_catalog_topk_workspace_ex(300, 5, 64, 64, 4082, 1 << 17, 0,

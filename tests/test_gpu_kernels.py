@@ -496,3 +496,79 @@ def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact):
         swaps = topk_tie_swaps(res["1"][1], ri + 5000, exact_fn)
         print(f"{dtype} {mode} exact={exact} K={K}: {swaps} verified fp32 tie swaps")
         assert swaps <= 8
+
+
+@pytest.mark.parametrize("mode", ["hhfm", "fm"])
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("k,K,B,n_item,exact", [
+    (64, 20, 3000, 4082, False),      # C3 itself: the default at >= 1,024 queries
+    (64, 20, 300, 4082, False),       # the reference's 300-row call (PLAN_FUSED)
+    (16, 1, 33, 700, False),          # K = 1, one partial workgroup range, 33 queries
+    (32, 32, 70, 5000, False),        # K = 32 (the fused kernel's widest), 5 ranges
+    (128, 5, 64, 16384, False),       # wide rows (two tiles in flight), 16 ranges
+    (64, 20, 40, 4082, True),         # PLAN_EXACT_FP32 (fp32 MFMA chain)
+])
+def test_catalog_topk_fused_small_path(mode, dtype, k, K, B, n_item, exact):
+    """The fused small-catalog kernel (catalog_fused.h: scores kept in
+    registers, a group-maximum threshold, survivors sorted in LDS — no [B, N]
+    score matrix): bit-identical ids and scores to the score-matrix path
+    (PLAN_STORE), and within the top-K parity bar of the oracle."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(k + K + B)
+    n_user = 957
+    A, M = synth_rows(rng, B, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    w = rng.normal(0, 0.01, size=M).astype(np.float32)
+    Eg = _dev(E) if dtype == "f32" else _dev(E).to(torch.bfloat16)
+    if dtype == "bf16":
+        E = bf16_round(E)
+    m = ops.MODE_HHFM if mode == "hhfm" else ops.MODE_FM
+    base = ops.PLAN_EXACT_FP32 if exact else 0
+
+    def run(plan):
+        return ops.catalog_topk(_dev(A), Eg, m, K, n_user, n_item, 0,
+                                _dev(w) if mode == "fm" else None, 0, (2, 5), (0, 0),
+                                plan=base | plan)
+    s, i = run(ops.PLAN_FUSED)
+    s0, i0 = run(ops.PLAN_STORE)
+    assert torch.equal(i, i0) and torch.equal(s, s0)
+    if mode == "hhfm":
+        ref = orc.hhfm_catalog_scores(A, E, n_user, n_item, 3, 0)
+        scale, ex = _hhfm_scale(A, E, n_user, n_item), hhfm_exact(A, E, n_user)
+    else:
+        ref = orc.fm_catalog_scores(A, E, w, n_user, n_item)
+        scale, ex = np.abs(ref).max(1, keepdims=True) + 0.05, fm_exact(A, E, w, n_user)
+    assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale, ex) <= MAX_TIES
+
+
+@pytest.mark.parametrize("case", ["all_equal", "two_levels", "shard"])
+def test_catalog_topk_fused_ties_and_shards(case):
+    """Heavy exact ties make every item of a range survive the threshold: the
+    fused kernel raises it to the K-th best (score, index) pair and filters
+    again until the survivors fit, keeping tf.nn.top_k's lower-index-first
+    order; a ragged shard (nonzero row and global bases) ranks like the
+    score-matrix path."""
+    from hhfm_amd import ops
+    rng = np.random.default_rng(31)
+    n_user, n_item, k = 50, 4082, 32
+    A, M = synth_rows(rng, 45, n_user, n_item, (7, 2, 3))
+    E = table(rng, M, k)
+    lo, cnt, gbase = n_user, n_item, 0
+    if case == "all_equal":
+        E[n_user:n_user + n_item] = E[n_user + 5]
+    elif case == "two_levels":
+        E[n_user:n_user + n_item] = E[n_user + 5]
+        E[n_user + 3000:n_user + n_item] = 2 * E[n_user + 5]   # 1,082 tied at the top
+    else:
+        lo, cnt, gbase = n_user + 777, 3001, 777
+    outs = [ops.catalog_topk(_dev(A), _dev(E), ops.MODE_HHFM, 20, lo, cnt, gbase, None, 0,
+                             (2, 5), (0, 0), plan=p) for p in (ops.PLAN_FUSED, ops.PLAN_STORE)]
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
+    i = outs[0][1].cpu().numpy()
+    if case == "all_equal":
+        assert np.array_equal(i, np.tile(np.arange(20, dtype=np.int32), (45, 1)))
+    elif case == "two_levels":
+        h = orc._hybrid(E, A[:, 0], A[:, 2:])
+        top = (h @ E[n_user + 5]) > 0          # the doubled rows rank first iff h·e > 0
+        want = np.where(top[:, None], np.arange(3000, 3020), np.arange(20)).astype(np.int32)
+        assert np.array_equal(i, want)
