@@ -24,6 +24,13 @@ namespace hhfm {
 #ifndef HHFM_K1_CAP
 #define HHFM_K1_CAP 64
 #endif
+// diagnostic (timing only, wrong results; default 0): where the `w` gathers
+// are served from — 1: every w index folded into a 1 MB window (L2-resident),
+// 2: w index x 32 (every gather its own 128-B line of a 2 GB array: no reuse
+// in L2 or the Infinity Cache); scripts/diag/k1_wmap.sh
+#ifndef HHFM_K1_WMAP
+#define HHFM_K1_WMAP 0
+#endif
 #ifndef HHFM_K1_U5
 #define HHFM_K1_U5 5   // rows per lane in flight at F = 5
 #endif
@@ -112,7 +119,9 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
           int32_t my = id[u][0];
 #pragma unroll
           for (int f = 1; f < F; ++f) my = (fsel == f) ? id[u][f] : my;
-          const float wl = w[my];
+          const float wl = HHFM_K1_WMAP == 1   ? w[my & 0x3ffff]
+                           : HHFM_K1_WMAP == 2 ? w[(int64_t)my * 32]
+                                               : w[my];
           wv[u] += (fsel < F) ? wl : 0.f;
         }
       }
