@@ -1576,11 +1576,11 @@ extern "C" int hhfm_afm_catalog_topk_ex(const int32_t* qidx, int64_t B, int32_t 
     if (K <= 32)
       hipLaunchKernelGGL((topk_dense_kernel<32, 32>), dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
                          item_count, (int64_t)item_count, K, global_item_base,
-                         top_score + b0 * K, top_idx + b0 * K);
+                         top_score + b0 * K, top_idx + b0 * K, nullptr);
     else
       hipLaunchKernelGGL((topk_dense_kernel<64, 32>), dim3((unsigned)tblocks), dim3(256), 0, st, sc, nq,
                          item_count, (int64_t)item_count, K, global_item_base,
-                         top_score + b0 * K, top_idx + b0 * K);
+                         top_score + b0 * K, top_idx + b0 * K, nullptr);
   }
   return (int)hipGetLastError();
 }

@@ -41,12 +41,20 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 #ifndef HHFM_MAIN_TARGET_WG
 #define HHFM_MAIN_TARGET_WG 512   // workgroups the item splits aim for (256: 2.16, 512: 1.64, 768: 1.78, 1024: 1.72, 2048: 1.87 ms, C4 shard bf16)
 #endif
-// threshold seed, at most: items and score-matrix floats (fp32 / bf16
-// tables; C4 shard, 1,024 queries: bf16 48 K items 0.96 vs 32 K 0.99 ms, fp32
-// 32 K 1.70 vs 48 K 1.71, 16 K / 8 K seeds 12-24 % slower, 128 K 45 % slower:
-// profiles/r04_k2_seed_ab.txt)
-constexpr int64_t kSeedMax[2] = {32768, 49152};
-constexpr int64_t kSeedBudget[2] = {(int64_t)32 << 20, (int64_t)48 << 20};
+// threshold seed, at most (fp32 / bf16 tables): its items are scored by a
+// GMAX pass (per query and 32-item tile the largest score, no score matrix);
+// C4 shard, 1,024 queries: fp32 24 / 32 / 48 / 64 K items 1.726 / 1.70 /
+// 1.683 / 1.688 ms, bf16 32 / 48 / 64 / 72 K 0.910 / 0.861 / 0.857 / 0.849 ms
+// (profiles/r05_k2_seed_ab.txt)
+#ifndef HHFM_SEED_F32
+#define HHFM_SEED_F32 49152
+#endif
+#ifndef HHFM_SEED_BF16
+#define HHFM_SEED_BF16 73728
+#endif
+constexpr int64_t kSeedMax[2] = {HHFM_SEED_F32, HHFM_SEED_BF16};
+// scored query-item pairs of the seed, at most: the full seed up to 1,024 queries
+constexpr int64_t kSeedBudget[2] = {kSeedMax[0] * 1024, kSeedMax[1] * 1024};
 #ifndef HHFM_RING_PAIR
 #define HHFM_RING_PAIR 0   // 1: catalog_ring bf16 with one s_barrier per two tiles (6-slot ring; measured neutral at C4, 1.20 vs 1.21 ms)
 #endif
@@ -119,11 +127,6 @@ HHFM_DEV int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
-// Order-preserving float <-> int32 key (signed compare == float compare).
-HHFM_DEV int32_t fkey(float f) {
-  const int32_t b = __float_as_int(f);
-  return b >= 0 ? b : (b ^ 0x7fffffff);
-}
 HHFM_DEV float fkey_inv(int32_t k) { return __int_as_float(k >= 0 ? k : (k ^ 0x7fffffff)); }
 
 template <int KPAD>
@@ -155,7 +158,11 @@ HHFM_DEV void insert_one(float* ls, int32_t* li, float s, int32_t it, int K) {
 // out_s [B][ostride_b] (the small-catalog path's scores for topk_dense).  The
 // MFMA operands are swapped (queries as A, items as B) so a lane's column is
 // an item: each store instruction writes 32 consecutive items of a query row.
-template <bool BF16, int KT, int KPAD, bool FM, bool SPLIT, bool STORE = false>
+// GMAX: no selection — per query and 32-item tile the largest score, out_s
+// [B][ostride_b] column = tile (the threshold seed: the K-th largest of K
+// disjoint tiles' maxima is a score at least K items reach).  Selecting
+// layout, so every maximum is bit for bit a score the main pass computes.
+template <bool BF16, int KT, int KPAD, bool FM, bool SPLIT, bool STORE = false, bool GMAX = false>
 __global__ __launch_bounds__(256) void catalog_main(
     const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
     const char* __restrict__ E, int64_t item_row_begin, int32_t N,
@@ -167,8 +174,11 @@ __global__ __launch_bounds__(256) void catalog_main(
   constexpr int EPC = BF16 ? 8 : 4;            // k-elements per 16-B chunk
   constexpr int kBulkMin = 128;                // candidates/tile -> bulk merge
 
-  __shared__ float lst_s[4][kQPerWave * KPAD];
-  __shared__ int32_t lst_i[4][kQPerWave * KPAD];
+  // list stride KPAD + 1: lane j's read of entry LST j + K - 1 (per tile) hits
+  // distinct banks (at stride 32 / 64 all 32 lanes fall in 2 / 1 banks)
+  constexpr int LST = KPAD + 1;
+  __shared__ float lst_s[4][kQPerWave * LST];
+  __shared__ int32_t lst_i[4][kQPerWave * LST];
   __shared__ float tb[4][kQPerWave * kTile];
 
   const int wid = xcd_remap(blockIdx.x, gridDim.x);
@@ -189,7 +199,7 @@ __global__ __launch_bounds__(256) void catalog_main(
   float* ls = lst_s[wv];
   int32_t* li = lst_i[wv];
   float* T = tb[wv];
-  for (int x = l; x < kQPerWave * KPAD; x += kWave) {
+  for (int x = l; x < kQPerWave * LST && !STORE && !GMAX; x += kWave) {
     ls[x] = kNegInf;
     li[x] = kNoIdx;
   }
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(256) void catalog_main(
   auto tile_step = [&](const int tile, uint4 (&ar)[KT], float& wr) {
     // global threshold hint: load now, consume after the MFMA chain (STORE:
     // no selection, and the small-catalog path leaves gthr unset)
-    const int32_t gk = (!STORE && q < B) ? gthr[q] : 0;
+    const int32_t gk = (!STORE && !GMAX && q < B) ? gthr[q] : 0;
     f32x16 acc = {0};
     const int nxt = tile + PF < tb1 ? tile + PF : tile;
     float wcur = wr;
@@ -349,6 +359,18 @@ __global__ __launch_bounds__(256) void catalog_main(
       }
       return;
     }
+    if constexpr (GMAX) {   // lane (j, h): query q, items rows (r&3)+8(r>>2)+4h
+      const int ib = tile * kTile;
+      float m = kNegInf;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        m = ib + row < item_end ? fmaxf(m, acc[r]) : m;
+      }
+      m = fmaxf(m, shfl_f(m, l ^ 32));
+      if (h == 0 && q < B) out_s[q * ostride_b + tile] = m;
+      return;
+    }
     // ---- filter against the per-query K-th score ----
     // The threshold is the better of this split's K-th score and the best
     // K-th score any split has published for the query (gthr: monotone
@@ -397,7 +419,7 @@ __global__ __launch_bounds__(256) void catalog_main(
               __builtin_amdgcn_readlane(__float_as_int(acc[r]), L));
           const int row = (r & 3) + 8 * (r >> 2) + 4 * (L >> 5);
           const int qq = L & 31;
-          insert_one<KPAD>(ls + qq * KPAD, li + qq * KPAD, s, ibase + row, K);
+          insert_one<KPAD>(ls + qq * LST, li + qq * LST, s, ibase + row, K);
         }
       }
     } else {
@@ -421,12 +443,12 @@ __global__ __launch_bounds__(256) void catalog_main(
           float bs = shfl_f(s, 32 * hh + j);
           int32_t bi = shfl_i(it, 32 * hh + j);
           if (l >= 32) { bs = kNegInf; bi = kNoIdx; }
-          float as = l < KPAD ? ls[qq * KPAD + l] : kNegInf;
-          int32_t ai = l < KPAD ? li[qq * KPAD + l] : kNoIdx;
+          float as = l < KPAD ? ls[qq * LST + l] : kNegInf;
+          int32_t ai = l < KPAD ? li[qq * LST + l] : kNoIdx;
           merge_lists<KPAD>(as, ai, bs, bi);
           if (l < KPAD) {
-            ls[qq * KPAD + l] = as;
-            li[qq * KPAD + l] = ai;
+            ls[qq * LST + l] = as;
+            li[qq * LST + l] = ai;
           }
         }
       }
@@ -434,7 +456,7 @@ __global__ __launch_bounds__(256) void catalog_main(
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     if (q < B) {
-      const float kth = ls[j * KPAD + (K - 1)];
+      const float kth = ls[j * LST + (K - 1)];
       if (kth > thr) {
         thr = kth;
         if (h == 0) atomicMax(gthr + q, fkey(kth));   // publish for other splits
@@ -452,7 +474,7 @@ __global__ __launch_bounds__(256) void catalog_main(
 
 #undef HHFM_PASS
 #undef HHFM_PASSMASK
-  if constexpr (STORE) return;
+  if constexpr (STORE || GMAX) return;
   // ---- emit this split's sorted list per query ----
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
@@ -460,8 +482,8 @@ __global__ __launch_bounds__(256) void catalog_main(
     const int64_t b = q0 + qq;
     if (b >= B) break;
     if (l < K) {
-      const int32_t ii = li[qq * KPAD + l];
-      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * KPAD + l];
+      const int32_t ii = li[qq * LST + l];
+      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * LST + l];
       out_i[b * ostride_b + split * ostride_s + l] = ii == kNoIdx ? kNoIdx : ii + gbase;
     }
   }
@@ -493,6 +515,15 @@ __global__ __launch_bounds__(256) void catalog_main(
 // the threshold seed, which leaves a few insertions per query and split.
 // Used for K <= 32, bf16 k = 128 and fp32 k in {64, 128}.
 // ---------------------------------------------------------------------------
+#ifndef HHFM_RING_TIMING
+#define HHFM_RING_TIMING 0   // diagnostic build: per-phase s_memtime sums (hhfm_debug_ring_timing)
+#endif
+#if HHFM_RING_TIMING
+// [0] publish (vmcnt + barrier + staging issue), [1] MFMA chain to ballots,
+// [2] selection, [3] wave-tiles, [4] whole kernel per wave, [5] waves
+__device__ unsigned long long g_ring_t[8];
+#endif
+
 template <bool BF16, int KT, int NW>
 struct RingCfg {
   static constexpr int kRingWaves = NW;                      // waves (x 32 queries) per workgroup
@@ -501,13 +532,20 @@ struct RingCfg {
   static constexpr int kNU = BF16 ? KT : KT / 2;             // 16-k MFMA steps per tile
   static constexpr int kSlots = BF16 ? HHFM_RING_SLOTS : 2;
   static constexpr int kStageB = BF16 ? kSlots * kTileB : 2 * 3 * kNU * 1024;
-  static constexpr int kListB = kRingWaves * kQPerWave * 32 * 8;   // KPAD 32
+  // per-query lists of KPAD 32 at a stride of 33 entries: the per-tile read
+  // of every query's K-th entry (lane j: entry 33 j + K - 1) then hits 32
+  // banks, not 2 (a 16-way conflict per wave and tile at stride 32)
+  static constexpr int kLStride = 33;
+  static constexpr int kListB = kRingWaves * kQPerWave * kLStride * 8;
   static constexpr int kSmem = kStageB + kListB;
   static constexpr int kDma = BF16 ? KT / kRingWaves : 0;    // DMA instructions per wave and tile
   static constexpr int kUnits = BF16 ? 0 : (kNU + NW - 1) / NW;   // fp32 split units per lane
 };
 
-template <bool BF16, int KT, bool FM, int NW>
+// GMAX: no selection — per query and tile the largest score into out_s
+// [B][ostride_b] (the threshold seed, as catalog_main's GMAX: same products,
+// same bits as the selecting pass)
+template <bool BF16, int KT, bool FM, int NW, bool GMAX = false>
 __global__ __launch_bounds__(NW * 64) void catalog_ring(
     const float* __restrict__ H, const float* __restrict__ cst, int64_t B,
     const char* __restrict__ E, int64_t item_row_begin, int32_t N,
@@ -545,9 +583,10 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   const int tb1 = min(tb0 + tiles_per_split, ntiles);
   const int item_end = min(tb1 * kTile, N);
 
-  float* ls = lst_s + wv * (kQPerWave * KPAD);
-  int32_t* li = lst_i + wv * (kQPerWave * KPAD);
-  for (int x = l; x < kQPerWave * KPAD; x += kWave) {
+  constexpr int LST = Cfg::kLStride;
+  float* ls = lst_s + wv * (kQPerWave * LST);
+  int32_t* li = lst_i + wv * (kQPerWave * LST);
+  for (int x = l; x < kQPerWave * LST && !GMAX; x += kWave) {
     ls[x] = kNegInf;
     li[x] = kNoIdx;
   }
@@ -580,7 +619,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   // the threshold seed (and any K-th an earlier split published): read once —
   // behind the seed the per-split lists rarely beat it, so a per-tile reload
   // of the hint would only put a global load on every tile's critical path
-  float thr = (q < B) ? fkey_inv(gthr[q]) : __builtin_huge_valf();
+  float thr = (!GMAX && q < B) ? fkey_inv(gthr[q]) : __builtin_huge_valf();
 
   auto item_row = [&](int tile, int jj) -> const char* {
     tile = tile < tb1 ? tile : tb1 - 1;
@@ -675,9 +714,16 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   // one tile: raw sets (cur holds tile+1's unit, nxt receives tile+3's) for fp32
   // sync: publish the stage (every fp32 tile; bf16 pairs: the first tile of
   // each pair, whose barrier also covers the second)
-  auto tile_step = [&](const int tile, uint4 (&cur)[NUL][2], uint4 (&nxt)[NUL][2],
-                       const bool sync) {
+#if HHFM_RING_TIMING
+  uint64_t tm_k0 = __builtin_amdgcn_s_memtime(), tm1 = 0, sum_pub = 0, sum_mma = 0,
+           sum_sel = 0, ntl = 0;
+#endif
+  // one tile = publish (sync: the stage is complete and the previous one
+  // free), score (the MFMA chain; acc = this wave's 32 items x 32 queries),
+  // select (filter + insert into the per-query lists)
+  auto publish = [&](const int tile, uint4 (&cur)[NUL][2], const bool sync) {
     const int it = tile - tb0;
+    (void)it;
     // ---- publish: tile's stage complete and the previous tile's stage free ----
     if (sync) {
       // bf16: every step issues its DMAs unconditionally (tiles past the split
@@ -701,7 +747,9 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
         if (tile + 3 < tb1) load_unit(tile + 3, cur);
       }
     }
-    (void)nxt;
+  };
+  auto score = [&](const int tile) -> f32x16 {
+    const int it = tile - tb0;
     float wcur = wnext;
     if constexpr (FM) {
       const int item = min((tile + 1 < tb1 ? tile + 1 : tile) * kTile + j, N - 1);
@@ -735,7 +783,22 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
     if constexpr (FM)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f, h == 0 ? 1.f : cq, acc,
                                                  0, 0, 0);
+    return acc;
+  };
+  auto select = [&](const int tile, const f32x16& acc) {
     if (!wave_live) return;
+    if constexpr (GMAX) {
+      const int ib = tile * kTile;
+      float m = kNegInf;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        m = ib + row < item_end ? fmaxf(m, acc[r]) : m;
+      }
+      m = fmaxf(m, shfl_f(m, l ^ 32));
+      if (h == 0 && q < B) out_s[q * ostride_b + tile] = m;
+      return;
+    }
     // ---- filter + insert: catalog_main's selection ----
     const int ibase = tile * kTile;
     uint64_t pm[16];
@@ -762,33 +825,57 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
         const float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc[r]), L));
         const int row = (r & 3) + 8 * (r >> 2) + 4 * (L >> 5);
         const int qq = L & 31;
-        insert_one<KPAD>(ls + qq * KPAD, li + qq * KPAD, s, ibase + row, K);
+        insert_one<KPAD>(ls + qq * LST, li + qq * LST, s, ibase + row, K);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     if (q < B) {
-      const float kth = ls[j * KPAD + (K - 1)];
+      const float kth = ls[j * LST + (K - 1)];
       if (kth > thr) {
         thr = kth;
         if (h == 0) atomicMax(gthr + q, fkey(kth));
       }
     }
   };
+#if HHFM_RING_TIMING
+#define HHFM_RING_T(x) x
+#else
+#define HHFM_RING_T(x)
+#endif
+  auto step = [&](const int tile, uint4 (&cur)[NUL][2], const bool sync) {
+    HHFM_RING_T(const uint64_t t0 = __builtin_amdgcn_s_memtime();)
+    publish(tile, cur, sync);
+    HHFM_RING_T(tm1 = __builtin_amdgcn_s_memtime();)
+    select(tile, score(tile));
+    HHFM_RING_T(sum_pub += tm1 - t0; sum_mma += __builtin_amdgcn_s_memtime() - tm1; ++ntl;)
+  };
+  // raw sets alternate by tile (compile-time register arrays: two steps per trip)
   for (int tile = tb0; tile < tb1; tile += 2) {
-    tile_step(tile, rawB, rawA, true);
-    if (tile + 1 < tb1) tile_step(tile + 1, rawA, rawB, !kPair);
+    step(tile, rawB, true);
+    if (tile + 1 < tb1) step(tile + 1, rawA, !kPair);
   }
+#undef HHFM_RING_T
 #undef HHFM_VMCNT
-  if (!wave_live) return;
+#if HHFM_RING_TIMING
+  if (wave_live && l == 0) {
+    atomicAdd(&g_ring_t[0], sum_pub);
+    atomicAdd(&g_ring_t[1], sum_mma);
+    atomicAdd(&g_ring_t[2], sum_sel);
+    atomicAdd(&g_ring_t[3], ntl);
+    atomicAdd(&g_ring_t[4], __builtin_amdgcn_s_memtime() - tm_k0);
+    atomicAdd(&g_ring_t[5], 1ull);
+  }
+#endif
+  if (!wave_live || GMAX) return;
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __builtin_amdgcn_wave_barrier();
   for (int qq = 0; qq < kQPerWave; ++qq) {
     const int64_t b = q0 + qq;
     if (b >= B) break;
     if (l < K) {
-      const int32_t ii = li[qq * KPAD + l];
-      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * KPAD + l];
+      const int32_t ii = li[qq * LST + l];
+      out_s[b * ostride_b + split * ostride_s + l] = ls[qq * LST + l];
       out_i[b * ostride_b + split * ostride_s + l] = ii == kNoIdx ? kNoIdx : ii + gbase;
     }
   }
@@ -879,6 +966,7 @@ struct Plan {
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
   int fS, fT;            // fused small-catalog kernel: workgroups per 32 queries, tiles per wave
   int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
+  int sS[2], stps[2];            // the same over the seed's items (its GMAX pass)
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
       off_seed_i, total;
 };
@@ -893,6 +981,16 @@ static bool dense_catalog(int64_t B, int32_t N) {
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// catalog_ring item splits: ~2 x 4-wave (v = 0) or 1 x 8-wave (v = 1)
+// workgroups per CU over nqb query groups, >= 16 tiles per split
+static void ring_splits(int nqb, int v, int ntiles, int& S, int& tps) {
+  const int smax = ntiles / 16 > 1 ? ntiles / 16 : 1;
+  int rs = ((512 >> v) + nqb - 1) / nqb;
+  rs = rs > smax ? smax : (rs < 1 ? 1 : rs);
+  tps = (ntiles + rs - 1) / rs;
+  S = (ntiles + tps - 1) / tps;
+}
 
 // Threshold seed of the streaming path (default on; HHFM_PLAN_NO_SEED off):
 // the exact top-K of the first seed_n items (STORE score matrix + dense
@@ -923,10 +1021,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
   for (int v = 0; v < 2; ++v) {   // catalog_ring: 2 x 4-wave or 1 x 8-wave workgroups per CU
     const int nq = 128 << v;
     p.rnqb[v] = (int)((B + nq - 1) / nq);
-    int rs = ((512 >> v) + p.rnqb[v] - 1) / p.rnqb[v];
-    rs = rs > smax ? smax : (rs < 1 ? 1 : rs);
-    p.rtps[v] = (ntiles + rs - 1) / rs;
-    p.rS[v] = (ntiles + p.rtps[v] - 1) / p.rtps[v];
+    ring_splits(p.rnqb[v], v, ntiles, p.rS[v], p.rtps[v]);
   }
   const int nsplit = std::max(p.S, std::max(p.rS[0], p.rS[1]));
   size_t off = 0;
@@ -960,7 +1055,7 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
   if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
-  // seed: up to kSeedMax items and a kSeedBudget-float score matrix, only when
+  // seed: up to kSeedMax items and kSeedBudget query-item pairs, only when
   // the catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
   p.seed_n = 0;
   if (!p.dense && !(plan & HHFM_PLAN_NO_SEED)) {
@@ -968,9 +1063,13 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
     sn = (sn > kSeedMax[bf16] ? kSeedMax[bf16] : sn) & ~int64_t(31);
     if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
   }
+  for (int v = 0; v < 2; ++v) {
+    p.sS[v] = p.stps[v] = 0;
+    if (p.seed_n) ring_splits(p.rnqb[v], v, p.seed_n / kTile, p.sS[v], p.stps[v]);
+  }
   p.off_seed_sc = off;
-  if (p.seed_n) {
-    off += align256((size_t)B * p.seed_n * sizeof(float));
+  if (p.seed_n) {   // the seed's tile maxima [B][seed_n / 32], their top-K lists
+    off += align256((size_t)B * (p.seed_n / kTile) * sizeof(float));
     p.off_seed_s = off;
     off += align256((size_t)B * K * sizeof(float));
     p.off_seed_i = off;
@@ -1030,6 +1129,37 @@ static bool dispatch_ring(int KT, const Plan& p, const float* H, const float* cs
     case 16:
       if constexpr (BF16) return false;
       else launch_ring<BF16, 16, FM>(p, H, cst, B, E, irb, N, w, K, os, oi, sb, ss, gbase, gthr, plan, st);
+      break;
+    default: return false;
+  }
+  return true;
+}
+
+// the threshold seed's tile maxima on catalog_ring (GMAX) over the first
+// seed_n items, when the main pass runs on the ring too
+template <bool BF16, int KT, bool FM>
+static void launch_ring_gmax(const Plan& p, const float* H, const float* cst, int64_t B,
+                             const char* E, int64_t irb, const float* w, float* gm, int64_t ldg,
+                             int32_t plan, hipStream_t st) {
+  if (ring_waves(BF16, plan) == 8)
+    hipLaunchKernelGGL((catalog_ring<BF16, KT, FM, 8, true>), dim3(p.rnqb[1] * p.sS[1]), dim3(512),
+                       0, st, H, cst, B, E, irb, p.seed_n, w, 1, p.sS[1], p.stps[1], p.rnqb[1], gm,
+                       nullptr, ldg, 0, 0, nullptr);
+  else
+    hipLaunchKernelGGL((catalog_ring<BF16, KT, FM, 4, true>), dim3(p.rnqb[0] * p.sS[0]), dim3(256),
+                       0, st, H, cst, B, E, irb, p.seed_n, w, 1, p.sS[0], p.stps[0], p.rnqb[0], gm,
+                       nullptr, ldg, 0, 0, nullptr);
+}
+
+template <bool BF16, bool FM>
+static bool dispatch_ring_gmax(int KT, const Plan& p, const float* H, const float* cst, int64_t B,
+                               const char* E, int64_t irb, const float* w, float* gm, int64_t ldg,
+                               int32_t plan, hipStream_t st) {
+  switch (KT) {
+    case 8: launch_ring_gmax<BF16, 8, FM>(p, H, cst, B, E, irb, w, gm, ldg, plan, st); break;
+    case 16:
+      if constexpr (BF16) return false;
+      else launch_ring_gmax<BF16, 16, FM>(p, H, cst, B, E, irb, w, gm, ldg, plan, st);
       break;
     default: return false;
   }
@@ -1123,6 +1253,43 @@ static bool dispatch_fused(int KT, int T, int64_t B, int nqb, int S, const int32
   return true;
 }
 
+// threshold seed on the catalog kernel (GMAX): per query and 32-item tile
+// the largest score into gm [B][ldg], ~2,048 workgroups like STORE
+template <bool BF16, int KT, bool FM>
+static void launch_gmax(int64_t B, int nqb, int32_t N, const float* H, const float* cst,
+                        const char* E, int64_t irb, const float* w, float* gm, int64_t ldg,
+                        int32_t plan, hipStream_t st) {
+  const int ntiles = (N + kTile - 1) / kTile;
+  int S = (HHFM_STORE_WG + nqb - 1) / nqb;
+  S = S > ntiles ? ntiles : (S < 1 ? 1 : S);
+  const int tps = (ntiles + S - 1) / S;
+  S = (ntiles + tps - 1) / tps;
+  constexpr bool kCanSplit = BF16 || KT >= 2;
+  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
+    hipLaunchKernelGGL((catalog_main<BF16, KT, 32, FM, kCanSplit, false, true>), dim3(nqb * S),
+                       dim3(256), 0, st, H, cst, B, E, irb, N, w, 1, S, tps, nqb, gm, nullptr,
+                       ldg, 0, 0, nullptr);
+  else
+    hipLaunchKernelGGL((catalog_main<BF16, KT, 32, FM, false, false, true>), dim3(nqb * S),
+                       dim3(256), 0, st, H, cst, B, E, irb, N, w, 1, S, tps, nqb, gm, nullptr,
+                       ldg, 0, 0, nullptr);
+}
+
+template <bool BF16, bool FM>
+static bool dispatch_gmax(int KT, int64_t B, int nqb, int32_t N, const float* H, const float* cst,
+                          const char* E, int64_t irb, const float* w, float* gm, int64_t ldg,
+                          int32_t plan, hipStream_t st) {
+  switch (KT) {
+    case 1: launch_gmax<BF16, 1, FM>(B, nqb, N, H, cst, E, irb, w, gm, ldg, plan, st); break;
+    case 2: launch_gmax<BF16, 2, FM>(B, nqb, N, H, cst, E, irb, w, gm, ldg, plan, st); break;
+    case 4: launch_gmax<BF16, 4, FM>(B, nqb, N, H, cst, E, irb, w, gm, ldg, plan, st); break;
+    case 8: launch_gmax<BF16, 8, FM>(B, nqb, N, H, cst, E, irb, w, gm, ldg, plan, st); break;
+    case 16: launch_gmax<BF16, 16, FM>(B, nqb, N, H, cst, E, irb, w, gm, ldg, plan, st); break;
+    default: return false;
+  }
+  return true;
+}
+
 template <bool BF16, bool FM>
 static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H,
                            const float* cst, const char* E, int64_t irb, const float* w,
@@ -1136,14 +1303,6 @@ static bool dispatch_store(int KT, int64_t B, int nqb, int32_t N, const float* H
     default: return false;
   }
   return true;
-}
-
-// gthr[b] = key of query b's K-th seed score (the seed's lists are sorted)
-__global__ __launch_bounds__(256) void seed_thr_kernel(const float* __restrict__ seed_s,
-                                                       int64_t B, int K,
-                                                       int32_t* __restrict__ gthr) {
-  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (b < B) gthr[b] = fkey(seed_s[b * K + (K - 1)]);
 }
 
 static void launch_merge(const float* in_s, const int32_t* in_i, int R, int64_t B,
@@ -1312,8 +1471,9 @@ extern "C" int hhfm_catalog_topk_ex(
     return (int)hipGetLastError();
   }
 
-  {   // streaming path only: the per-query threshold hints start below every
-    // score (0x80808080 decodes to ~-3.4e38); the dense path never reads them
+  if (!p.seed_n) {   // streaming path without a seed: the per-query threshold
+    // hints start below every score (0x80808080 decodes to ~-3.4e38); the
+    // seed writes every b < B, the only hints the kernels read
     const hipError_t me = hipMemsetAsync(gthr, 0x80, (size_t)p.Bpad * sizeof(int32_t), st);
     if (me != hipSuccess) return (int)me;
   }
@@ -1344,14 +1504,23 @@ extern "C" int hhfm_catalog_topk_ex(
     int32_t* sdi = reinterpret_cast<int32_t*>(ws + p.off_seed_i);
     const float* wv = (fm && w) ? w : nullptr;
     const int64_t irb = item_row_begin;
-    if (bf16) ok = fm ? dispatch_store<true, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st)
-                      : dispatch_store<true, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st);
-    else ok = fm ? dispatch_store<false, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st)
-                 : dispatch_store<false, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, p.seed_n, gthr, plan, st);
+    const int32_t G = p.seed_n / kTile;   // tiles of the seed (>= 128 >= K)
+    // the tile maxima on the kernel the main pass runs on (bit-identical scores)
+    if (ring) {
+      if (bf16) ok = fm ? dispatch_ring_gmax<true, true>(KT, p, H, cst, B, Eb, irb, wv, ssc, G, plan, st)
+                        : dispatch_ring_gmax<true, false>(KT, p, H, cst, B, Eb, irb, wv, ssc, G, plan, st);
+      else ok = fm ? dispatch_ring_gmax<false, true>(KT, p, H, cst, B, Eb, irb, wv, ssc, G, plan, st)
+                   : dispatch_ring_gmax<false, false>(KT, p, H, cst, B, Eb, irb, wv, ssc, G, plan, st);
+    } else if (bf16) {
+      ok = fm ? dispatch_gmax<true, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, G, plan, st)
+              : dispatch_gmax<true, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, G, plan, st);
+    } else {
+      ok = fm ? dispatch_gmax<false, true>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, G, plan, st)
+              : dispatch_gmax<false, false>(KT, B, p.nqb, p.seed_n, H, cst, Eb, irb, wv, ssc, G, plan, st);
+    }
     if (!ok) return HHFM_EUNSUPPORTED;
-    launch_topk_dense(ssc, B, p.seed_n, p.seed_n, K, 0, sds, sdi, st);
-    hipLaunchKernelGGL(seed_thr_kernel, dim3((int)((B + 255) / 256)), dim3(256), 0, st, sds, B,
-                       K, gthr);
+    // gthr[b] = key of the K-th largest tile maximum
+    launch_topk_dense(ssc, B, G, G, K, 0, sds, sdi, st, false, gthr);
   }
 #define HHFM_MAIN_ARGS KT, p, H, cst, B, Eb, (int64_t)item_row_begin, item_count, w, K, os, oi, sb, ss, gbase, gthr, plan, st
   if (ring) {
@@ -1372,6 +1541,16 @@ extern "C" int hhfm_catalog_topk_ex(
   }
   return (int)hipGetLastError();
 }
+
+#if HHFM_RING_TIMING
+// diagnostic builds only: read and clear the ring kernel's phase sums
+extern "C" int hhfm_debug_ring_timing(unsigned long long* out) {
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ring_t), sizeof(g_ring_t)) != hipSuccess) return -1;
+  static const unsigned long long zero[8] = {0};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ring_t), zero, sizeof(zero));
+}
+#endif
 
 extern "C" int hhfm_topk_merge(const float* in_score, const int32_t* in_idx,
                                int32_t R, int64_t B, int32_t K, float* out_score,

@@ -193,12 +193,20 @@ HHFM_DEV void topk_fold_chunk(const float (&v)[NV], const float* src, int32_t cb
   thr = fmaxf(thr, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ls), K - 1)));
 }
 
+// Order-preserving float -> int32 key (signed compare == float compare).
+HHFM_DEV int32_t fkey(float f) {
+  const int32_t b = __float_as_int(f);
+  return b >= 0 ? b : (b ^ 0x7fffffff);
+}
+
+// kth (optional): kth[b] = fkey of query b's K-th score (the threshold seed)
 template <int KPAD, int NV>
 __global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict__ S,
                                                          int64_t B, int32_t N, int64_t lds,
                                                          int K, int32_t base,
                                                          float* __restrict__ out_s,
-                                                         int32_t* __restrict__ out_i) {
+                                                         int32_t* __restrict__ out_i,
+                                                         int32_t* __restrict__ kth) {
   __shared__ float cand_s[4][kWave];
   __shared__ int32_t cand_i[4][kWave];
   const int l = lane_id(), wv = (threadIdx.x >> 6) & 3;
@@ -221,6 +229,7 @@ __global__ __launch_bounds__(256) void topk_dense_kernel(const float* __restrict
     if (l < K) {
       out_s[b * K + l] = ls;
       out_i[b * K + l] = li == kNoIdx ? kNoIdx : li + base;
+      if (kth && l == K - 1) kth[b] = fkey(ls);
     }
   }
 }
@@ -236,7 +245,8 @@ __global__ __launch_bounds__(256) void topk_dense_split_kernel(const float* __re
                                                                int64_t B, int32_t N, int64_t lds,
                                                                int K, int32_t base,
                                                                float* __restrict__ out_s,
-                                                               int32_t* __restrict__ out_i) {
+                                                               int32_t* __restrict__ out_i,
+                                                               int32_t* __restrict__ kth) {
   constexpr int QB = 4 / WPQ;   // queries per workgroup
   __shared__ float cand_s[4][kWave];
   __shared__ int32_t cand_i[4][kWave];
@@ -281,6 +291,7 @@ __global__ __launch_bounds__(256) void topk_dense_split_kernel(const float* __re
       if (l < K) {
         out_s[b * K + l] = ls;
         out_i[b * K + l] = li == kNoIdx ? kNoIdx : li + base;
+        if (kth && l == K - 1) kth[b] = fkey(ls);
       }
     }
     __syncthreads();   // ms / mi are rewritten by the next query group
@@ -298,7 +309,7 @@ static inline int topk_dense_wpq(int64_t B, int32_t N, bool one_wave) {
 
 static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64_t lds, int K,
                               int32_t base, float* os, int32_t* oi, hipStream_t st,
-                              bool one_wave = false) {
+                              bool one_wave = false, int32_t* kth = nullptr) {
   const int wpq = topk_dense_wpq(B, N, one_wave);
   if (wpq > 1) {
     const int qb = 4 / wpq;
@@ -306,7 +317,7 @@ static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64
     if (blocks > 8192) blocks = 8192;
 #define HHFM_TOPK_SPLIT(KP, W)                                                                   \
   hipLaunchKernelGGL((topk_dense_split_kernel<KP, HHFM_TOPK_NV, W>), dim3((int)blocks), dim3(256), 0, \
-                     st, S, B, N, lds, K, base, os, oi)
+                     st, S, B, N, lds, K, base, os, oi, kth)
     if (K <= 32) {
       if (wpq == 4) HHFM_TOPK_SPLIT(32, 4); else HHFM_TOPK_SPLIT(32, 2);
     } else {
@@ -320,10 +331,10 @@ static inline void launch_topk_dense(const float* S, int64_t B, int32_t N, int64
   if (blocks < 1) blocks = 1;
   if (K <= 32)
     hipLaunchKernelGGL((topk_dense_kernel<32, HHFM_TOPK_NV>), dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
-                       K, base, os, oi);
+                       K, base, os, oi, kth);
   else
     hipLaunchKernelGGL((topk_dense_kernel<64, HHFM_TOPK_NV>), dim3((int)blocks), dim3(256), 0, st, S, B, N, lds,
-                       K, base, os, oi);
+                       K, base, os, oi, kth);
 }
 
 }  // namespace hhfm
