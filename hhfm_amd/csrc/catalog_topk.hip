@@ -503,8 +503,8 @@ __global__ __launch_bounds__(256) void catalog_main(
 //     (global_load_lds_dwordx4) with per-lane source addresses chosen so the
 //     image is [k16 step][half][item] x 16 B — every A-operand ds_read_b128
 //     reads 16 consecutive 16-B slots (conflict-free);
-//   * fp32 tables: each lane loads NU/4 (item, 16-k step, half) units of the
-//     tile two tiles ahead into registers, splits them into their three bf16
+//   * fp32 tables: each lane loads NU/NW (item, 16-k step, half) units of the
+//     tile one tile ahead into registers, splits them into their three bf16
 //     pieces (exact, split3x8) and stores them into a double-buffered piece
 //     image [piece][step][half][item]: 1/256 of the split work per lane.
 // One s_barrier per tile (4 waves; the other workgroup on the CU is not
@@ -515,6 +515,11 @@ __global__ __launch_bounds__(256) void catalog_main(
 // the threshold seed, which leaves a few insertions per query and split.
 // Used for K <= 32, bf16 k = 128 and fp32 k in {64, 128}.
 // ---------------------------------------------------------------------------
+#ifndef HHFM_RING_KO
+// diagnostic knock-outs (wrong results; timing only): 1 no selection (scores
+// still consumed), 2 no per-tile s_barrier, 4 no MFMA chain
+#define HHFM_RING_KO 0
+#endif
 #ifndef HHFM_RING_TIMING
 #define HHFM_RING_TIMING 0   // diagnostic build: per-phase s_memtime sums (hhfm_debug_ring_timing)
 #endif
@@ -650,7 +655,9 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
 #pragma unroll
       for (int r = 0; r < NUL; ++r) {
         const int u = wv + kRingWaves * r;
-        if (u < NU) {
+        // (compile-time true when the waves divide the steps: no branch, so
+        // the compiler counts these loads exactly in its vmcnt waits)
+        if (NU % kRingWaves == 0 || u < NU) {
           raw[r][0] = *reinterpret_cast<const uint4*>(row + 64 * u);
           raw[r][1] = *reinterpret_cast<const uint4*>(row + 64 * u + 32);
         }
@@ -662,7 +669,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
 #pragma unroll
       for (int r = 0; r < NUL; ++r) {
         const int u = wv + kRingWaves * r;
-        if (u >= NU) continue;
+        if (NU % kRingWaves != 0 && u >= NU) continue;
         const float x[8] = {__uint_as_float(raw[r][0].x), __uint_as_float(raw[r][0].y),
                             __uint_as_float(raw[r][0].z), __uint_as_float(raw[r][0].w),
                             __uint_as_float(raw[r][1].x), __uint_as_float(raw[r][1].y),
@@ -690,16 +697,15 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
 #define HHFM_VMCNT(n) \
   __builtin_amdgcn_s_waitcnt(((n) & 0xF) | (((n) >> 4) << 14) | (0x7 << 4) | (0xF << 8))
 
-  uint4 rawA[NUL][2], rawB[NUL][2];
+  uint4 raw[NUL][2];
   float wnext = 0.f;
   if (tb0 < tb1) {
     if constexpr (BF16) {
       for (int s = 0; s < (kPair ? R - 2 : R - 1); ++s) dma_tile(tb0 + s, s);
     } else {
-      load_unit(tb0, rawA);
-      load_unit(tb0 + 1, rawB);
-      store_pieces(rawA, 0);          // waits for rawA (vmcnt counted by the compiler)
-      load_unit(tb0 + 2, rawA);
+      load_unit(tb0, raw);
+      store_pieces(raw, 0);
+      load_unit(tb0 + 1, raw);
     }
     if constexpr (FM) {
       const int item = min(tb0 * kTile + j, N - 1);
@@ -708,10 +714,16 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   }
 
   auto mma16 = [&](const bf16x8& x, const bf16x8& y, const f32x16& c) {
+#if HHFM_RING_KO & 4   // knock-out: the operands still read, no MFMA
+    f32x16 r = c;
+    r[0] += __builtin_bit_cast(float, __builtin_bit_cast(uint4, x).x) * 1e-30f;
+    (void)y;
+    return r;
+#else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(x, y, c, 0, 0, 0);
+#endif
   };
 
-  // one tile: raw sets (cur holds tile+1's unit, nxt receives tile+3's) for fp32
   // sync: publish the stage (every fp32 tile; bf16 pairs: the first tile of
   // each pair, whose barrier also covers the second)
 #if HHFM_RING_TIMING
@@ -721,7 +733,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   // one tile = publish (sync: the stage is complete and the previous one
   // free), score (the MFMA chain; acc = this wave's 32 items x 32 queries),
   // select (filter + insert into the per-query lists)
-  auto publish = [&](const int tile, uint4 (&cur)[NUL][2], const bool sync) {
+  auto publish = [&](const int tile, const bool sync) {
     const int it = tile - tb0;
     (void)it;
     // ---- publish: tile's stage complete and the previous tile's stage free ----
@@ -735,16 +747,18 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
       else if constexpr (BF16)
         HHFM_VMCNT((R - 2) * Cfg::kDma);
       __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's piece stores landed
-      __builtin_amdgcn_s_barrier();
+      if (!(HHFM_RING_KO & 2)) __builtin_amdgcn_s_barrier();
       if constexpr (kPair) {   // into the previous pair's slots
         dma_tile(tile + 4, (it + 4) % R);
         dma_tile(tile + 5, (it + 5) % R);
       } else if constexpr (BF16) {
         dma_tile(tile + R - 1, (it + R - 1) % R);
       } else {
-        // split tile+1 into the other piece buffer, then fetch tile+3's unit
-        if (tile + 1 < tb1) store_pieces(cur, (it + 1) & 1);
-        if (tile + 3 < tb1) load_unit(tile + 3, cur);
+        // split tile+1 into the other piece buffer, then fetch the unit of
+        // tile+2 into the same registers (one tile of lead), unconditionally:
+        // past the split's end load_unit re-reads its last tile
+        store_pieces(raw, (it + 1) & 1);
+        load_unit(tile + 2, raw);
       }
     }
   };
@@ -787,6 +801,15 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
   };
   auto select = [&](const int tile, const f32x16& acc) {
     if (!wave_live) return;
+#if HHFM_RING_KO & 1
+    {
+      float sx = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sx += acc[r];
+      if (sx == 1234.5f) out_s[0] = sx;
+      return;
+    }
+#endif
     if constexpr (GMAX) {
       const int ib = tile * kTile;
       float m = kNegInf;
@@ -796,7 +819,7 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
         m = ib + row < item_end ? fmaxf(m, acc[r]) : m;
       }
       m = fmaxf(m, shfl_f(m, l ^ 32));
-      if (h == 0 && q < B) out_s[q * ostride_b + tile] = m;
+      if (h == 0 && q < B && tile < tb1) out_s[q * ostride_b + tile] = m;
       return;
     }
     // ---- filter + insert: catalog_main's selection ----
@@ -843,18 +866,19 @@ __global__ __launch_bounds__(NW * 64) void catalog_ring(
 #else
 #define HHFM_RING_T(x)
 #endif
-  auto step = [&](const int tile, uint4 (&cur)[NUL][2], const bool sync) {
+  auto step = [&](const int tile, const bool sync) {
     HHFM_RING_T(const uint64_t t0 = __builtin_amdgcn_s_memtime();)
-    publish(tile, cur, sync);
+    publish(tile, sync);
     HHFM_RING_T(tm1 = __builtin_amdgcn_s_memtime();)
     select(tile, score(tile));
     HHFM_RING_T(sum_pub += tm1 - t0; sum_mma += __builtin_amdgcn_s_memtime() - tm1; ++ntl;)
   };
-  // raw sets alternate by tile (compile-time register arrays: two steps per trip)
-  for (int tile = tb0; tile < tb1; tile += 2) {
-    step(tile, rawB, true);
-    if (tile + 1 < tb1) step(tile + 1, rawA, !kPair);
-  }
+  // one raw register set, loaded one tile ahead (fp32).  Two sets
+  // alternating over an unrolled pair of steps (two tiles of lead) ran the
+  // same with unconditional loads (1.572 vs 1.571 ms) and 1.66 ms with the
+  // old conditional ones, whose registers the compiler rotated through copies
+  // behind a vmcnt(0) every second tile (profiles/r05_k2_c4.txt)
+  for (int tile = tb0; tile < tb1; ++tile) step(tile, !kPair || !((tile - tb0) & 1));
 #undef HHFM_RING_T
 #undef HHFM_VMCNT
 #if HHFM_RING_TIMING
