@@ -37,12 +37,17 @@ namespace hhfm {
 #ifndef HHFM_FUSED_KO
 #define HHFM_FUSED_KO 0
 #endif
-// diagnostic: s_memtime at the phase boundaries of workgroup 0, wave 0,
-// written over the first query's ids (timing only; 1 = on)
+// diagnostic: s_memtime at the phase boundaries, every wave's phase
+// durations summed into g_fused_t (read by hhfm_debug_fused_timing; timing
+// only; 1 = on)
 #ifndef HHFM_FUSED_TIMING
 #define HHFM_FUSED_TIMING 0
 #endif
 #if HHFM_FUSED_TIMING
+// [0..5] phases 0-1 (ids, query rows, LDS), 1-2 (B operands), 2-3 (scores),
+// 3-4 (threshold), 4-5 (survivors), 5-6 (sort, write); [6] waves; [7] sum of
+// the first mark's spread (wave start - earliest start is not known: raw start)
+__device__ unsigned long long g_fused_t[8];
 #define HHFM_TMARK(i) tmk[i] = __builtin_amdgcn_s_memtime()
 #else
 #define HHFM_TMARK(i) (void)0
@@ -55,7 +60,7 @@ constexpr int kFusedMaxCtx = 8;   // context (and time) fields the fused kernel 
 // of 4 tiles (two waves per SIMD within 256 registers) rather than 4 of 8 —
 // each wave's chain of dependent tile loads is half as long (4 x 8 measured
 // 50-60 us per call against ... with 8 x 4: profiles/r05_c3_fused_ab.txt)
-constexpr int kFusedWaves = 8, kFusedTiles = 4;   // tiles per wave: 4, or 8 for many queries
+constexpr int kFusedWaves = 8, kFusedTiles = 4;
 
 // bitonic sort of scores in aligned groups of N lanes (no indices: only the
 // K-th value is wanted)
@@ -140,6 +145,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   // 16 (T = 4) or 32 (T = 8) items each
   constexpr int TG = T / 4, NG = 64;
   static_assert(T == 4 || T == 8, "fused catalog kernel: 4 or 8 tiles per wave");
+  constexpr int NU = SPLIT ? (BF16 ? KT : KT / 2) : 1;
 
   __shared__ float hq[kQPerWave][k + 4];
   __shared__ float cq_l[kQPerWave];
@@ -149,9 +155,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   __shared__ int32_t thr_i[kQPerWave];
   __shared__ int32_t cnt[kQPerWave];
   __shared__ int32_t again;
-  // per query kFusedCap (score, index bits) slots + a spare, then one dummy
-  // slot per lane (the writes of rows that did not pass)
-  __shared__ float2 cbuf[kQPerWave * (kFusedCap + 1) + kFusedWaves * 64];
+  // per query kFusedCap (score, index bits) slots + a spare
+  __shared__ float2 cbuf[kQPerWave * (kFusedCap + 1)];
 
   const int g = blockIdx.x / S, split = blockIdx.x - (blockIdx.x / S) * S;
   const int wv = threadIdx.x / kWave;
@@ -231,8 +236,10 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       for (int c = 0; c < LPT; ++c)
 #pragma unroll
         for (int v = 0; v < EPC; ++v) part[c][v] = 0.f;
-      auto row = [&](int32_t id, int ch, float (&x)[EPC]) {
-        const uint4 u = *reinterpret_cast<const uint4*>(E + (int64_t)id * ROWB + 16 * ch);
+      // every field row of a chunk is loaded before any is summed (loads
+      // interleaved with the sums were each followed by a vmcnt(0): one
+      // memory latency per field, in series)
+      auto cvt = [&](const uint4& u, float (&x)[EPC]) {
         if constexpr (BF16) {
           const uint32_t r4[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
@@ -245,29 +252,42 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           x[2] = __uint_as_float(u.z); x[3] = __uint_as_float(u.w);
         }
       };
+      const int nc = c1 - c0, nt = t1 - t0;
 #pragma unroll
       for (int cc = 0; cc < CPT; ++cc) {
         const int ch = tp + 8 * cc;
         if (ch < CPR) {
+          auto ld = [&](int32_t id) {
+            return *reinterpret_cast<const uint4*>(E + (int64_t)id * ROWB + 16 * ch);
+          };
+          const uint4 ru = ld(idu);
+          uint4 rc[kFusedMaxCtx], rt[kFusedMaxCtx];
+#pragma unroll
+          for (int f = 0; f < kFusedMaxCtx; ++f) {
+            rc[f] = make_uint4(0, 0, 0, 0);
+            rt[f] = make_uint4(0, 0, 0, 0);
+            if (f < nc) rc[f] = ld(idc[f]);
+            if (f < nt) rt[f] = ld(idt[f]);
+          }
           float uu[EPC], cx[EPC], tm[EPC], r[EPC];
-          row(idu, ch, uu);
+          cvt(ru, uu);
 #pragma unroll
           for (int v = 0; v < EPC; ++v) {
             cx[v] = 0.f;
             tm[v] = 0.f;
           }
-          // ctx fields, then time fields: uniform trip counts (scalar branches)
+          // ctx fields, then time fields, in field order: uniform trip counts
 #pragma unroll
           for (int f = 0; f < kFusedMaxCtx; ++f) {
-            if (f >= c1 - c0) break;
-            row(idc[f], ch, r);
+            if (f >= nc) break;
+            cvt(rc[f], r);
 #pragma unroll
             for (int v = 0; v < EPC; ++v) cx[v] += r[v];
           }
 #pragma unroll
           for (int f = 0; f < kFusedMaxCtx; ++f) {
-            if (f >= t1 - t0) break;
-            row(idt[f], ch, r);
+            if (f >= nt) break;
+            cvt(rt[f], r);
 #pragma unroll
             for (int v = 0; v < EPC; ++v) tm[v] += r[v];
           }
@@ -308,6 +328,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     }
   }
   if (threadIdx.x < kQPerWave) cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) again = 0;
   __syncthreads();
   HHFM_TMARK(1);
 
@@ -317,7 +338,6 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   for (int t = 0; t < KT; ++t)
 #pragma unroll
     for (int e = 0; e < EPC; ++e) bq[t][e] = hq[j][(2 * t + h) * EPC + e];
-  constexpr int NU = SPLIT ? (BF16 ? KT : KT / 2) : 1;
   bf16x8 qp[3][NU];
   if constexpr (SPLIT) {
 #pragma unroll
@@ -331,9 +351,17 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       split3x8(x, qp[0][u], qp[1][u], qp[2][u]);
     }
   }
+  auto QP = [&](int pc, int u) -> bf16x8 { return qp[pc][u]; };
   const float cq = FM ? cq_l[j] : 0.f;
 
   HHFM_TMARK(2);
+#if HHFM_FUSED_KO & 8   // knock-out: stop after the query phase (tile loads consumed)
+  {
+    float z = __uint_as_float(ar[0][0].x) + __uint_as_float(QP(0, 0)[0]);
+    if (z == 1234.5f) out_s[0] = z;
+    return;
+  }
+#endif
   // ---- 1. scores of this wave's T tiles, kept in registers ----
   float sc[T][16];
 #pragma unroll
@@ -352,7 +380,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     if constexpr (HHFM_FUSED_KO & 4) {
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
-        acc[t] += __uint_as_float(ar_[t].x) * (float)qp[0][0][t & 7];
+        acc[t] += __uint_as_float(ar_[t].x) * (float)QP(0, 0)[t & 7];
         if (refill) ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
       }
     } else if constexpr (SPLIT && BF16) {
@@ -360,9 +388,9 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       for (int t = 0; t < KT; ++t) {
         const bf16x8 ai = __builtin_bit_cast(bf16x8, ar_[t]);
         if (refill) ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[2][t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[1][t], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[0][t], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(2, t), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(1, t), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(0, t), acc, 0, 0, 0);
       }
     } else if constexpr (SPLIT) {
 #pragma unroll
@@ -375,12 +403,13 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         if (refill) ar_[2 * u + 1] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u + 1));
         bf16x8 i0, i1, i2;
         split3x8(x, i0, i1, i2);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, qp[0][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[1][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[2][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, qp[0][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[1][u], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, qp[0][u], acc, 0, 0, 0);
+        const bf16x8 q0 = QP(0, u), q1 = QP(1, u), q2 = QP(2, u);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, q0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, q1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q2, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, q0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q1, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q0, acc, 0, 0, 0);
       }
     } else {
 #pragma unroll
@@ -523,23 +552,22 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     int pos = n ? atomicAdd(&cnt[j], n) : 0;
     HHFM_TMARK(8);
     asm volatile("" : "+v"(ib));   // recompute the indices below (no 16 T live values)
-    // branch-free writes of (score, index) as one 8-B slot: a row that did
-    // not pass writes the lane's dummy slot, slots past the list's end the
-    // query's spare slot kFusedCap (the address picked arithmetically, so no
-    // per-row lane masks stay live)
+    // (score, index) as one 8-B slot; slots past the list's end go to the
+    // query's spare slot kFusedCap
     constexpr int kQS = kFusedCap + 1;   // slots per query (the last: spare)
-    const int dummy = kQPerWave * kQS + wv * 64 + l;
     const int qbase = j * kQS;
 #pragma unroll
     for (int tt = 0; tt < T; ++tt) {
       const uint32_t m = pm[tt];
       if (__ballot(m != 0) != 0) {
+        // only the passing rows write (exec-masked stores; branch-free
+        // writes of every row to a dummy slot measured 2 % slower)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const bool pb = (m >> r) & 1u;
-          const int real = qbase + min(pos, kFusedCap);
-          cbuf[pb ? real : dummy] =
-              make_float2(sc[tt][r], __int_as_float(ib + tt * kTile + (r & 3) + 8 * (r >> 2)));
+          if (pb)
+            cbuf[qbase + min(pos, kFusedCap)] =
+                make_float2(sc[tt][r], __int_as_float(ib + tt * kTile + (r & 3) + 8 * (r >> 2)));
           pos += pb ? 1 : 0;
         }
       }
@@ -548,9 +576,12 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       asm volatile("" : "+v"(pos) : : "memory");
     }
     HHFM_TMARK(9);
-    if (threadIdx.x == 0) again = 0;
+    // a lane whose last slot lies past the cap flags the overflow: the
+    // common case (no list overflowed) then costs one barrier
+    if (pos > kFusedCap) again = 1;
     __syncthreads();
     HHFM_TMARK(10);
+    if (!again) break;
     // overflowed queries: the K-th best pair among the kFusedCap collected
     // becomes the threshold (at least K items reach it), and the range is
     // filtered again from an empty list
@@ -568,14 +599,13 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         thr_s[qq] = ns;
         thr_i[qq] = ni;
         cnt[qq] = -1;   // marks: filter this query again
-        again = 1;
       }
     }
     __syncthreads();
-    if (!again) break;
     // queries not overflowed keep their lists: their lanes add nothing
     const bool redo = cnt[j] < 0;
     __syncthreads();
+    if (threadIdx.x == 0) again = 0;
     if (threadIdx.x < kQPerWave && cnt[threadIdx.x] < 0) cnt[threadIdx.x] = 0;
     if (!redo) {
       thr_s[j] = __builtin_huge_valf();   // (written by both lanes of j: same value)
@@ -622,6 +652,36 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
 #pragma unroll 1
       for (int qi = 0; qi < 2 * PW; ++qi) {
         const int qq = 2 * (wv + NW * (qi >> 1)) + (qi & 1), nq = cnt[qq];
+        // per pair: a pair whose lists both fit 32 lanes takes the 32-lane
+        // network (its second query is done with the first); a list of at
+        // most 64 one 64-lane sort
+        const int qo = qq ^ 1, no = cnt[qo];
+        if (nq <= 32 && no <= 32) {
+          if (qi & 1) continue;   // done with its pair
+          const int qh = qq + h, nh = h ? no : nq;
+          const float2 e = cbuf[qh * (kFusedCap + 1) + (j < nh ? j : 0)];
+          float sv[1] = {j < nh ? e.x : kNegInf};
+          int32_t iv[1] = {j < nh ? __float_as_int(e.y) : kNoIdx};
+          bitonic_sort_desc_n<32, 1>(sv, iv);
+          const int64_t b = q0 + qh;
+          if (b < B && j < K) {
+            out_s[b * ostride_b + ob + j] = sv[0];
+            out_i[b * ostride_b + ob + j] = iv[0] == kNoIdx ? kNoIdx : iv[0] + gbase;
+          }
+          continue;
+        }
+        if (nq <= 64) {
+          const float2 e = cbuf[qq * (kFusedCap + 1) + (l < nq ? l : 0)];
+          float s1 = l < nq ? e.x : kNegInf;
+          int32_t i1 = l < nq ? __float_as_int(e.y) : kNoIdx;
+          bitonic_sort_desc<64>(s1, i1);
+          const int64_t b = q0 + qq;
+          if (b < B && l < K) {
+            out_s[b * ostride_b + ob + l] = s1;
+            out_i[b * ostride_b + ob + l] = i1 == kNoIdx ? kNoIdx : i1 + gbase;
+          }
+          continue;
+        }
         float ls = kNegInf;
         int32_t li = kNoIdx;
 #pragma unroll 1
@@ -646,8 +706,15 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   }
 #if HHFM_FUSED_TIMING
   HHFM_TMARK(6);
-  if (blockIdx.x == 0 && threadIdx.x == 0)
-    for (int i = 0; i < 11; ++i) out_i[i] = (int32_t)(tmk[i] - tmk[0]);
+  if (l == 0) {
+    atomicAdd(&g_fused_t[0], tmk[1] - tmk[0]);
+    atomicAdd(&g_fused_t[1], tmk[2] - tmk[1]);
+    atomicAdd(&g_fused_t[2], tmk[3] - tmk[2]);
+    atomicAdd(&g_fused_t[3], tmk[4] - tmk[3]);
+    atomicAdd(&g_fused_t[4], tmk[5] - tmk[4]);
+    atomicAdd(&g_fused_t[5], tmk[6] - tmk[5]);
+    atomicAdd(&g_fused_t[6], 1ull);
+  }
 #endif
 }
 

@@ -1061,14 +1061,14 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
     p.off_pi = off;
   }
   // the fused small-catalog kernel (catalog_fused.h): S_f workgroups per
-  // 32 queries, each kFusedWaves waves x kFusedTiles tiles; S_f > 1 merges
-  // lists of K from off_ps
+  // 32 queries, each kFusedWaves waves x T tiles; S_f > 1 merges lists of K
+  // from off_ps.  (8 tiles per wave — half the workgroups, one round on the
+  // CUs at 3,000 queries — ran 4 % faster at C3 but spills 150 B of
+  // registers per lane: not kept, profiles/r05_c3_fused.txt)
   {
-    constexpr int kTilesWG = kFusedWaves * kFusedTiles;
-    p.fS = (ntiles + kTilesWG - 1) / kTilesWG;
-    // (8 tiles per wave, half the workgroups, spilled ~150 registers: not kept)
+    const int fS4 = (ntiles + kFusedWaves * kFusedTiles - 1) / (kFusedWaves * kFusedTiles);
     p.fT = kFusedTiles;
-    const int fS4 = p.fS;
+    p.fS = fS4;
     if (p.dense && fS4 > 1 && nsplit < fS4) {
       off = p.off_ps;
       off += align256((size_t)B * fS4 * K * sizeof(float));
@@ -1565,6 +1565,16 @@ extern "C" int hhfm_catalog_topk_ex(
   }
   return (int)hipGetLastError();
 }
+
+#if HHFM_FUSED_TIMING
+// diagnostic builds only: read and clear the fused kernel's phase sums
+extern "C" int hhfm_debug_fused_timing(unsigned long long* out) {
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(g_fused_t)) != hipSuccess) return -1;
+  static const unsigned long long zero[8] = {0};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_t), zero, sizeof(zero));
+}
+#endif
 
 #if HHFM_RING_TIMING
 // diagnostic builds only: read and clear the ring kernel's phase sums

@@ -4,8 +4,10 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/c3paths
-for B in 3000 300; do
-  for plan in 0 8192; do
+# CASES: "B:plan ..." (plan 16384 = HHFM_PLAN_FUSED, 8192 = HHFM_PLAN_STORE)
+for case in ${CASES:-3000:0 3000:8192 300:16384 300:8192}; do
+  B=${case%%:*}; plan=${case##*:}
+  for once in 1; do
     rm -rf gpurun_out/c3paths/b${B}_p$plan
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/c3paths/b${B}_p$plan -o k --output-format csv -- python scripts/diag/c3_one.py $B $plan > /dev/null 2> gpurun_out/c3paths/b${B}_p$plan.err || { echo "failed"; tail -3 gpurun_out/c3paths/b${B}_p$plan.err; exit 1; }
     python3 - $B $plan <<'PY'

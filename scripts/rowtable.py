@@ -309,7 +309,7 @@ if not only or "h35" in only:
     n = X.shape[0] * 50
     res["H5_sample_negative"] = {
         "config": f"sample_negative(Train rows, 50) on a Frappe-shape split ({X.shape[0]:,} rows; "
-                  "evaluate_AUC's draw), numpy RNG on the host, membership on the device",
+                  "evaluate_AUC's draw), the whole sampler on the device (hhfm_sample_negative: MT19937 stream, masked draws, membership, re-draws)",
         "unit": "samples/s", "gpu_ms_wall": t_dev * 1e3, "gpu_rate": n / t_dev,
         "cpu_rate_numpy": n / t_host,
         "cpu_sample": "same call, host harness (vectorised membership, same stream)"}
