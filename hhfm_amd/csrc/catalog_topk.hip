@@ -1079,13 +1079,16 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
   if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
-  // seed: up to kSeedMax items and kSeedBudget query-item pairs, only when
-  // the catalog is >= 16x the seed (the seed pass then costs <= ~6 % of the MFMA work)
+  // seed: up to kSeedMax items, kSeedBudget query-item pairs and 1/16 of the
+  // catalog (the seed pass then costs <= ~6 % of the MFMA work); none below
+  // 4,096 items (catalogs under 65,536 items)
   p.seed_n = 0;
   if (!p.dense && !(plan & HHFM_PLAN_NO_SEED)) {
     int64_t sn = kSeedBudget[bf16] / p.Bpad;
-    sn = (sn > kSeedMax[bf16] ? kSeedMax[bf16] : sn) & ~int64_t(31);
-    if (sn >= 4096 && (int64_t)N >= 16 * sn) p.seed_n = (int)sn;
+    sn = sn > kSeedMax[bf16] ? kSeedMax[bf16] : sn;
+    sn = sn > (int64_t)N / 16 ? (int64_t)N / 16 : sn;
+    sn &= ~int64_t(31);
+    if (sn >= 4096) p.seed_n = (int)sn;
   }
   for (int v = 0; v < 2; ++v) {
     p.sS[v] = p.stps[v] = 0;

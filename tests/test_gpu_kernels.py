@@ -446,8 +446,9 @@ def test_catalog_topk_c4_shard(dtype):
 @pytest.mark.parametrize("mode", ["hhfm", "fm"])
 @pytest.mark.parametrize("dtype,k", [("f32", 128), ("bf16", 64), ("bf16", 128)])
 def test_catalog_topk_threshold_seed_is_exact(dtype, k, mode, exact):
-    """The streaming path's threshold seed (exact top-K of the first 32,768
-    items from the STORE score matrix) only drops items that cannot reach the
+    """The streaming path's threshold seed (the K-th largest per-tile score
+    maximum over the first catalog/16 items, here 37,472, on the main pass's
+    own kernel) only drops items that cannot reach the
     top-K: seeded and unseeded (PLAN_NO_SEED) runs return the same bits, and
     both match the C oracle (shard with non-zero row and global bases, K = 20
     and 64); where the ring kernel runs, catalog_main (PLAN_NO_RING) and the
@@ -541,7 +542,7 @@ def test_catalog_topk_fused_small_path(mode, dtype, k, K, B, n_item, exact):
     assert _check_topk(ref, s.cpu().numpy(), i.cpu().numpy(), K, scale, ex) <= MAX_TIES
 
 
-@pytest.mark.parametrize("case", ["all_equal", "two_levels", "shard"])
+@pytest.mark.parametrize("case", ["all_equal", "two_levels", "shard", "tied50", "tied90"])
 def test_catalog_topk_fused_ties_and_shards(case):
     """Heavy exact ties make every item of a range survive the threshold: the
     fused kernel raises it to the K-th best (score, index) pair and filters
@@ -559,6 +560,12 @@ def test_catalog_topk_fused_ties_and_shards(case):
     elif case == "two_levels":
         E[n_user:n_user + n_item] = E[n_user + 5]
         E[n_user + 3000:n_user + n_item] = 2 * E[n_user + 5]   # 1,082 tied at the top
+    elif case in ("tied50", "tied90"):
+        # 50 / 90 exact ties at the top of one workgroup range for queries with
+        # h·e > 0: 33-64 survivors take the one 64-lane sort, more the chunked
+        # sort + merge loop (catalog_fused.h phase 4)
+        nt = 50 if case == "tied50" else 90
+        E[n_user + 100:n_user + 100 + nt] = 4 * E[n_user + 5]
     else:
         lo, cnt, gbase = n_user + 777, 3001, 777
     outs = [ops.catalog_topk(_dev(A), _dev(E), ops.MODE_HHFM, 20, lo, cnt, gbase, None, 0,
