@@ -1,4 +1,5 @@
-"""Item-sharded full-catalog top-K across the GPUs of a node.
+"""Item-sharded full-catalog top-K across the GPUs of a node,
+and row-sharded per-row scoring / metrics.
 
 The reference ranks the whole catalog on one device with one tf.nn.top_k
 (FM.py:185, OurModel7.py:295).  Here, one process per GPU:
@@ -163,3 +164,41 @@ def sharded_evaluate_auc(tr, data1, group=None) -> float:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return float(t[0] / t[1])
+
+
+# ---------------------------------------------------------------------------
+# Row-sharded per-row scores (C2 / C5 over N GPUs: rows split, no exchange in
+# the data path; one gather only when the caller wants every score on every rank)
+# ---------------------------------------------------------------------------
+RowScorer = Callable[[object], torch.Tensor]
+
+
+def sharded_score_rows(X, score_rows: RowScorer, gather: bool = True, group=None):
+    """``sess.run(model.out)`` (FM.py:99-120, DFM.py:104-137, AFM.py:103-142)
+    over a batch shared by every rank, its rows split across the ranks: rank r
+    scores the contiguous rows ``shard_range(len(X), world, r)`` with
+    ``score_rows`` (e.g. ``model.score_rows`` — the HIP row kernels on the
+    rank's GPU) and, with ``gather``, one all-gather of the per-rank float32
+    slices (padded to the longest) returns every row's score in row order on
+    every rank — the single-device result, since a row's score never depends
+    on the others.  ``gather=False`` returns (this rank's scores, begin)."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    n = len(X)
+    b, e = shard_range(n, world, rank)
+    dev = comm_device(group)
+    mine = (torch.as_tensor(np.asarray(score_rows(X[b:e])), dtype=torch.float32).reshape(-1)
+            if e > b else torch.empty(0, dtype=torch.float32))
+    mine = mine.to(dev)
+    if not gather:
+        return mine, b
+    if world == 1:
+        return mine
+    longest = shard_range(n, world, 0)[1]          # rank 0 holds the longest slice
+    pad = torch.zeros(longest, dtype=torch.float32, device=dev)
+    pad[:mine.numel()] = mine
+    out = torch.empty(world * longest, dtype=torch.float32, device=dev)
+    dist.all_gather_into_tensor(out, pad, group=group)
+    out = out.view(world, longest)
+    return torch.cat([out[r, :shard_range(n, world, r)[1] - shard_range(n, world, r)[0]]
+                      for r in range(world)])
