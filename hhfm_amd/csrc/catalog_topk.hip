@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) void catalog_main(
 // One s_barrier per tile (4 waves; the other workgroup on the CU is not
 // coupled to it).  The MFMA products, their k order and the selection are
 // catalog_main's (SPLIT path), so scores are bit-identical to it and to the
-// STORE seed.  Candidates are inserted one by one (the dense sort + merge
+// GMAX seed.  Candidates are inserted one by one (the dense sort + merge
 // path and its LDS transpose buffer are dropped): the kernel runs only behind
 // the threshold seed, which leaves a few insertions per query and split.
 // Used for K <= 32, bf16 k = 128 and fp32 k in {64, 128}.
@@ -1017,16 +1017,17 @@ static void ring_splits(int nqb, int v, int ntiles, int& S, int& tps) {
 }
 
 // Threshold seed of the streaming path (default on; HHFM_PLAN_NO_SEED off):
-// the exact top-K of the first seed_n items (STORE score matrix + dense
-// top-K) gives every query a K-th score t before the main pass.  K catalog
-// items score >= t, so the global K-th is >= t and items below t can be
-// dropped; without it every item split warms its lists up from -inf and the
-// per-split thresholds (and their atomicMax hint, a max of per-split K-ths)
-// stay near the K-th of one split, which costs ~K·ln(items per split / K)
-// list insertions per query and split.  The STORE kernel computes every
-// score with the same MFMA products in the same k order as the selecting
-// kernel (operands swapped: D = Aᵀ-layout), so t is bit-exactly a score the
-// main pass reproduces (tests/test_gpu_kernels.py: seeded == unseeded).
+// the first seed_n items are scored by the main pass's own kernel in its GMAX
+// form (per query and 32-item tile only the tile's maximum), and the dense
+// top-K over those seed_n / 32 maxima writes every query's K-th one, t, as
+// its threshold hint before the main pass.  K distinct catalog items score
+// >= t, so the global K-th is >= t and items below t can be dropped; without
+// it every item split warms its lists up from -inf and the per-split
+// thresholds (and their atomicMax hint, a max of per-split K-ths) stay near
+// the K-th of one split, which costs ~K·ln(items per split / K) list
+// insertions per query and split.  The GMAX pass computes every score with
+// the main pass's products in the same k order, so t is bit-exactly a score
+// the main pass reproduces (tests/test_gpu_kernels.py: seeded == unseeded).
 static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, bool bf16) {
   Plan p{};
   p.nqb = (int)((B + kQPerBlock - 1) / kQPerBlock);
