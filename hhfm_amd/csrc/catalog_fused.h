@@ -1,84 +1,84 @@
 // K2 small-catalog path (C3: evaluate_TopK over Frappe's 4,082 items;
 // Newcode/OurModel7.py:294-295, FM.py:180-185): scores + exact top-K in ONE
-// kernel, the [B, N] score matrix never written.  Included by
+// kernel launch — the [B, N] score matrix is never written and the split
+// lists are merged inside the launch (no topk_merge kernel).  Included by
 // catalog_topk.hip (uses its tile constants, split-bf16 helpers and the
 // wave-level top-K primitives of topk_common.h).
 //
-// A workgroup = 8 waves = 32 queries x a range of 8·T item tiles (S
-// workgroups per query group cover the catalog; their lists are merged by
-// topk_merge, S = 1 writes the final lists).
+// S workgroups per 32 queries, each = 8 waves x one range of 8·T item tiles
+// (wave w takes the range's tiles [w·T, w·T + T)):
 //   0. the 32 query vectors formed in LDS (catalog_queries' arithmetic), each
 //      wave's MFMA B operands built from them (catalog_main's split pieces);
+//      the wave's first item tiles are already in flight;
 //   1. every wave scores its T tiles with catalog_main's exact MFMA sequence
 //      (same products, same order: the same bits as the selecting and STORE
-//      kernels) and KEEPS the T x 16 scores of its lanes in registers;
-//   2. threshold: every (lane half, tile) is a group of 16 items of one query,
-//      8T groups per query in the workgroup.  The K-th largest group maximum
-//      t is a lower bound of the query's K-th best score in the range (K
-//      distinct groups hold a score >= t), so every item of the range's
-//      top-K scores >= t — while only ~K·(1 + small) items do (K = 20, 64
-//      groups: ~24 of 1,024);
-//   3. the survivors (score >= t) go to a per-query LDS list (slot from an
-//      LDS counter); more than kFusedCap of them (heavy exact ties) raises
-//      the threshold to the K-th best (score, index) PAIR among those
-//      collected and filters again — each round drops at least kFusedCap - K
-//      items, so it ends, and the pair order keeps tf.nn.top_k's ties;
-//   4. per query the survivors are sorted by one bitonic network (32 lanes,
-//      two queries per wave, or 64-lane chunks merged into the list) and the
-//      top K written.
-// Exactness: the candidates are a superset of the range's top K under the
-// strict (score desc, index asc) order, so the lists equal the dense path's.
+//      kernels) and keeps the T x 16 scores of its lanes in registers;
+//   2. threshold: every (wave, lane half, tile) is a group of 16 items of one
+//      query.  Each lane offers its two largest tile maxima, 32 values per
+//      query; their K-th largest t is the maximum of K distinct groups, so K
+//      items of the range score >= t (~K·1.2 of a 1,024-item range do);
+//   3. the survivors (score >= t) go to a per-query LDS list.  A list past
+//      kFusedCap (heavy exact ties) raises the threshold to the K-th best
+//      (score, index) PAIR among those collected and filters again — each
+//      round drops at least kFusedCap - K items, so it ends, and the pair
+//      order keeps tf.nn.top_k's ties;
+//   4. per query the entries at or above the final threshold are sorted by
+//      one 32-lane key network: the range's exact top K;
+//   5. S > 1: the sorted lists are stored write-through (sc1), every storing
+//      wave drains, and one lane adds to the query group's arrival counter
+//      (agent scope); the workgroup whose add comes last loads the S lists
+//      with sc1 loads, merges them and writes the top K, then re-arms the
+//      counter (MI355X_MICROARCH.md § visibility, the first row of the
+//      hand-off table; no fence, no second launch).
+// Exactness: every range contributes a superset of its top K under the strict
+// (score desc, index asc) order, so the lists equal the dense path's.
+//
+// Selection arithmetic is branch-free on the VALU: entries are 64-bit keys
+// compared by v_cmp_u64 (the (score, index) pair compare compiled to
+// SALU/exec-mask sequences that cost ~20 cycles per instruction here), the
+// survivors leave registers through a select tree, and barriers are LDS-only
+// (the item tiles in flight stay in flight across them).
 #pragma once
 
 namespace hhfm {
 
-// diagnostic knock-outs (timing only, wrong results; default 0): 1 no
-// survivor phases (3-4), 2 no threshold phase either, 4 no MFMAs
-#ifndef HHFM_FUSED_KO
-#define HHFM_FUSED_KO 0
-#endif
 // diagnostic: s_memtime at the phase boundaries, every wave's phase
 // durations summed into g_fused_t (read by hhfm_debug_fused_timing; timing
 // only; 1 = on)
 #ifndef HHFM_FUSED_TIMING
 #define HHFM_FUSED_TIMING 0
 #endif
+#if HHFM_FUSED_TIMING && !defined(HHFM_DIAG_BUILD)
+#error "HHFM_FUSED_TIMING: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
 #if HHFM_FUSED_TIMING
-// [0..5] phases 0-1 (ids, query rows, LDS), 1-2 (B operands), 2-3 (scores),
-// 3-4 (threshold), 4-5 (survivors), 5-6 (sort, write); [6] waves; [7] sum of
-// the first mark's spread (wave start - earliest start is not known: raw start)
+// [0] query phase, [1] scores, [2] threshold, [3] survivors (+ overflow
+// rounds), [4] range sort and hand-off, [5] waves, [6] merging workgroups,
+// [7] merge
 __device__ unsigned long long g_fused_t[8];
-#define HHFM_TMARK(i) tmk[i] = __builtin_amdgcn_s_memtime()
+#define HHFM_TMARK(v) v = __builtin_amdgcn_s_memtime()
 #else
-#define HHFM_TMARK(i) (void)0
+#define HHFM_TMARK(v) (void)0
 #endif
 
-constexpr int kFusedCap = 128;   // survivors held per query and workgroup
+constexpr int kFusedCap = 128;    // list entries held per query
+// arrival counters (one per 32 queries) at the workspace's start
+constexpr int kFusedMaxGroups = HHFM_CATALOG_WS_ZERO / 4;
+constexpr int kFusedMaxS = 16;    // item ranges (workgroups) per 32 queries
+constexpr int kFusedTiles = 4;    // item tiles per wave: a range = 8 x 4 tiles = 1,024 items
 constexpr int kFusedMaxCtx = 8;   // context (and time) fields the fused kernel takes
+constexpr int kFusedWaves = 8;
 
-// waves per workgroup and tiles per wave: a lane keeps T x 16 scores; 8 waves
-// of 4 tiles (two waves per SIMD within 256 registers) rather than 4 of 8 —
-// each wave's chain of dependent tile loads is half as long (4 x 8 measured
-// 50-60 us per call against ... with 8 x 4: profiles/r05_c3_fused_ab.txt)
-constexpr int kFusedWaves = 8, kFusedTiles = 4;
-
-// bitonic sort of scores in aligned groups of N lanes (no indices: only the
-// K-th value is wanted)
-template <int N>
-HHFM_DEV void sort_desc_scores(float& s) {
-  const int l = lane_id() & (N - 1);
-#pragma unroll
-  for (int size = 2; size <= N; size <<= 1) {
-    const bool desc = (l & size) == 0 || size == N;
-#pragma unroll
-    for (int d = size >> 1; d >= 1; d >>= 1) {
-      const float ps = xor_lane(s, d);
-      s = (((l & d) == 0) == desc) ? fmaxf(s, ps) : fminf(s, ps);
-    }
-  }
+// workgroup barrier that orders LDS only: outstanding global loads (the next
+// item tiles) stay in flight across it (__syncthreads waits for them)
+HHFM_DEV void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// Q independent score sorts (one per register), interleaved stage by stage
+// bitonic sort of scores in aligned groups of N lanes (no indices: only the
+// K-th value is wanted), Q independent sorts interleaved stage by stage
 template <int N, int Q>
 HHFM_DEV void sort_desc_scores_n(float (&s)[Q]) {
   const int l = lane_id() & (N - 1);
@@ -97,79 +97,119 @@ HHFM_DEV void sort_desc_scores_n(float (&s)[Q]) {
   }
 }
 
-// Q independent (score, index) bitonic sorts in aligned groups of N lanes,
-// interleaved stage by stage (tf.nn.top_k order, as bitonic_sort_desc)
-template <int N, int Q>
-HHFM_DEV void bitonic_sort_desc_n(float (&s)[Q], int32_t (&i)[Q]) {
+// Entry keys: one uint64 per (score, index), larger = better under the
+// strict (score desc, index asc) order of tf.nn.top_k — the high word the
+// order-preserving bits of the score, the low word ~index.  Compares and
+// swaps are then a v_cmp_u64 and two v_cndmask (no exec-mask branches: the
+// (score, index) pair compare compiled to SALU/exec sequences that cost
+// ~20 cycles per instruction here).  Key 0 is below every entry (empty).
+HHFM_DEV uint32_t ukey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return b ^ ((uint32_t)((int32_t)b >> 31) | 0x80000000u);
+}
+HHFM_DEV float ukey_inv(uint32_t k) {
+  return __uint_as_float(k ^ ((k & 0x80000000u) ? 0x80000000u : 0xffffffffu));
+}
+HHFM_DEV uint64_t ekey(float s, int32_t i) {
+  return ((uint64_t)ukey(s) << 32) | (uint32_t)~i;
+}
+HHFM_DEV uint64_t xor_lane64(uint64_t v, int d) {
+  const uint32_t lo = (uint32_t)xor_lane((int32_t)(uint32_t)v, d);
+  const uint32_t hi = (uint32_t)xor_lane((int32_t)(uint32_t)(v >> 32), d);
+  return ((uint64_t)hi << 32) | lo;
+}
+// bitonic sort of keys, descending, in aligned groups of N lanes
+template <int N>
+HHFM_DEV void sort_keys_desc(uint64_t& k) {
   const int l = lane_id() & (N - 1);
 #pragma unroll
   for (int size = 2; size <= N; size <<= 1) {
     const bool desc = (l & size) == 0 || size == N;
 #pragma unroll
     for (int d = size >> 1; d >= 1; d >>= 1) {
-      const bool keep_better = ((l & d) == 0) == desc;
-      float ps[Q];
-      int32_t pi[Q];
-#pragma unroll
-      for (int u = 0; u < Q; ++u) {
-        ps[u] = xor_lane(s[u], d);
-        pi[u] = xor_lane(i[u], d);
-      }
-#pragma unroll
-      for (int u = 0; u < Q; ++u) {
-        const bool pb = better(ps[u], pi[u], s[u], i[u]);
-        const bool take = keep_better ? pb : !pb;
-        s[u] = take ? ps[u] : s[u];
-        i[u] = take ? pi[u] : i[u];
-      }
+      const uint64_t p = xor_lane64(k, d);
+      const bool keep_max = ((l & d) == 0) == desc;
+      k = ((p > k) == keep_max) ? p : k;
     }
   }
 }
-
-// pass (score, index) at or above the pair threshold (ts, ti): better or equal
-HHFM_DEV bool at_least(float s, int32_t i, float ts, int32_t ti) {
-  return s > ts || (s == ts && i <= ti);
+// the best N of the union of two descending key lists A (self) and B, in
+// aligned groups of N lanes: max(A[l], B[N-1-l]) is bitonic, then merged
+template <int N>
+HHFM_DEV void merge_keys(uint64_t& a, uint64_t b) {
+  const int l = lane_id();
+  const int src = (l & ~(N - 1)) | (N - 1 - (l & (N - 1)));
+  const uint32_t blo = (uint32_t)__shfl((int32_t)(uint32_t)b, src, kWave);
+  const uint32_t bhi = (uint32_t)__shfl((int32_t)(uint32_t)(b >> 32), src, kWave);
+  const uint64_t r = ((uint64_t)bhi << 32) | blo;
+  a = r > a ? r : a;
+  const int lg = l & (N - 1);
+#pragma unroll
+  for (int d = N >> 1; d >= 1; d >>= 1) {
+    const uint64_t p = xor_lane64(a, d);
+    a = ((p > a) == ((lg & d) == 0)) ? p : a;
+  }
+}
+// v[r] for a lane-dependent r in [0, 16): a 4-level tree of bitwise blends
+// (v_bfi_b32).  Written as selects, the compiler turns them into a load
+// through a selected address and moves the score array to scratch.
+HHFM_DEV float select16(const float (&v)[16], int r) {
+  auto bl = [](uint32_t a, uint32_t b, uint32_t m) { return (b & m) | (a & ~m); };
+  const uint32_t m0 = 0u - (uint32_t)(r & 1), m1 = 0u - (uint32_t)((r >> 1) & 1);
+  const uint32_t m2 = 0u - (uint32_t)((r >> 2) & 1), m3 = 0u - (uint32_t)((r >> 3) & 1);
+  uint32_t a[8], b[4], c[2];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) a[x] = bl(__float_as_uint(v[2 * x]), __float_as_uint(v[2 * x + 1]), m0);
+#pragma unroll
+  for (int x = 0; x < 4; ++x) b[x] = bl(a[2 * x], a[2 * x + 1], m1);
+#pragma unroll
+  for (int x = 0; x < 2; ++x) c[x] = bl(b[2 * x], b[2 * x + 1], m2);
+  return __uint_as_float(bl(c[0], c[1], m3));
 }
 
 template <bool BF16, int KT, bool FM, bool SPLIT, int T>
 __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     const int32_t* __restrict__ qidx, int64_t B, int ncols, int mode, int ucol, int c0, int c1,
     int t0, int t1, const char* __restrict__ E, int64_t M, int64_t item_row_begin, int32_t N,
-    const float* __restrict__ w, int K, int S, float* __restrict__ out_s,
-    int32_t* __restrict__ out_i, int64_t ostride_b, int64_t ostride_s, int32_t gbase) {
+    const float* __restrict__ w, int K, float* __restrict__ out_s, int32_t* __restrict__ out_i,
+    int32_t gbase, int S, uint32_t* __restrict__ arrive, uint64_t* __restrict__ part) {
   constexpr int k = BF16 ? KT * 16 : KT * 8;
   constexpr int64_t ROWB = (int64_t)KT * 32;
   constexpr int EPC = BF16 ? 8 : 4;
   constexpr int NW = kFusedWaves;
-  // groups per query: every (wave, lane half, run of T/4 tiles) — 64 groups,
-  // 16 (T = 4) or 32 (T = 8) items each
-  constexpr int TG = T / 4, NG = 64;
-  static_assert(T == 4 || T == 8, "fused catalog kernel: 4 or 8 tiles per wave");
   constexpr int NU = SPLIT ? (BF16 ? KT : KT / 2) : 1;
+  constexpr int R = 32 / (2 * NW);     // tile maxima a lane offers
+  constexpr int kQS = kFusedCap + 1;   // list slots per query (the last: spare)
+  // item tiles in flight per wave (one for bf16 k >= 128: its 96 registers of
+  // query pieces leave no room for a second)
+  constexpr int PD = BF16 && KT >= 8 ? 1 : 2;
+  static_assert(T % PD == 0, "tiles per wave a multiple of the prefetch depth");
 
   __shared__ float hq[kQPerWave][k + 4];
   __shared__ float cq_l[kQPerWave];
   __shared__ float pq[kQPerWave][64];   // FM: per query, catalog_queries' 64 lane values
-  __shared__ float gmax[kQPerWave][64];
-  __shared__ float thr_s[kQPerWave];
-  __shared__ int32_t thr_i[kQPerWave];
-  __shared__ int32_t cnt[kQPerWave];
-  __shared__ int32_t again;
-  // per query kFusedCap (score, index bits) slots + a spare
-  __shared__ float2 cbuf[kQPerWave * (kFusedCap + 1)];
+  __shared__ float gmx[kQPerWave][33];  // per query the 32 offered group values
+  __shared__ uint64_t thr_k[kQPerWave];   // entries with a key >= pass
+  __shared__ int32_t cnt[kQPerWave], cprev[kQPerWave], redo[kQPerWave];
+  __shared__ int32_t ovf[2];
+  __shared__ uint64_t cbuf[kQPerWave * kQS];   // entry keys
+  __shared__ uint64_t fscr[NW][kWave];         // range sort: compacted keys
+  __shared__ int32_t last_sh;                  // this workgroup merges its group
 
-  const int g = blockIdx.x / S, split = blockIdx.x - (blockIdx.x / S) * S;
   const int wv = threadIdx.x / kWave;
   const int l = lane_id();
   const int j = l & 31, h = l >> 5;
+  const int g = blockIdx.x / S, split = blockIdx.x - (blockIdx.x / S) * S;
   const int64_t q0 = (int64_t)g * kQPerWave;
+  const bool live = q0 + j < B;   // this lane's query exists (rows past B add nothing)
   const int ntiles = (N + kTile - 1) / kTile;
-  const int tile0 = (split * NW + wv) * T;
+  const int tile0 = (split * NW + wv) * T;   // this wave's first tile
+  int rnd = 0;   // survivor rounds so far (selects the overflow flag word)
 
 #if HHFM_FUSED_TIMING
-  uint64_t tmk[12] = {};
+  uint64_t tm0 = 0, tm1 = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
 #endif
-  HHFM_TMARK(0);
+  HHFM_TMARK(tm0);
   // the query rows' raw ids first (8 threads per query; only the first 256
   // threads form queries): their loads are the oldest, so waiting for them
   // leaves the tile loads below in flight (vmcnt counts in order)
@@ -189,15 +229,18 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     }
   }
   asm volatile("" ::: "memory");   // keep the tile loads behind them
-  // item operands of the wave's first PD tiles (all T when they fit in 64
-  // registers), issued before the query phase so their latency overlaps it
-  constexpr int PD = KT <= 4 && T <= 4 ? T : 2;
-  uint4 ar[PD][KT];
-  float wr[PD];
+  // the wave's tile tt -> catalog tile (clamped: every load is issued, so
+  // the counted waits stay exact)
+  auto tile_of = [&](int tt) {
+    const int t = tile0 + (tt < T ? tt : T - 1);
+    return t < ntiles ? t : ntiles - 1;
+  };
   auto item_of = [&](int tile) {
-    int item = tile * kTile + j;
+    const int item = tile * kTile + j;
     return item < N ? item : N - 1;
   };
+  uint4 ar[PD][KT];
+  float wr[PD];
   auto load_tile = [&](int tile, uint4 (&a)[KT], float& wv_) {
     const char* row = E + (item_row_begin + item_of(tile)) * ROWB + 16 * h;
 #pragma unroll
@@ -207,7 +250,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
 #pragma unroll
   for (int d = 0; d < PD; ++d) {
     wr[d] = 0.f;
-    load_tile(tile0 + d < ntiles ? tile0 + d : ntiles - 1, ar[d], wr[d]);
+    load_tile(tile_of(d), ar[d], wr[d]);
   }
 
   // ---- 0. query vectors (catalog_queries' arithmetic, bit for bit) ----
@@ -236,9 +279,6 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       for (int c = 0; c < LPT; ++c)
 #pragma unroll
         for (int v = 0; v < EPC; ++v) part[c][v] = 0.f;
-      // every field row of a chunk is loaded before any is summed (loads
-      // interleaved with the sums were each followed by a vmcnt(0): one
-      // memory latency per field, in series)
       auto cvt = [&](const uint4& u, float (&x)[EPC]) {
         if constexpr (BF16) {
           const uint32_t r4[4] = {u.x, u.y, u.z, u.w};
@@ -260,6 +300,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           auto ld = [&](int32_t id) {
             return *reinterpret_cast<const uint4*>(E + (int64_t)id * ROWB + 16 * ch);
           };
+          // every field row of a chunk loaded before any is summed (one memory
+          // latency, not one per field)
           const uint4 ru = ld(idu);
           uint4 rc[kFusedMaxCtx], rt[kFusedMaxCtx];
 #pragma unroll
@@ -276,7 +318,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
             cx[v] = 0.f;
             tm[v] = 0.f;
           }
-          // ctx fields, then time fields, in field order: uniform trip counts
+          // ctx fields, then time fields, in field order
 #pragma unroll
           for (int f = 0; f < kFusedMaxCtx; ++f) {
             if (f >= nc) break;
@@ -318,19 +360,22 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         }
       }
     }
-    __syncthreads();
+    if (threadIdx.x < kQPerWave) {
+      cnt[threadIdx.x] = 0;
+      // the lowest finite score: items past N (held as -inf) never pass
+      thr_k[threadIdx.x] = (uint64_t)ukey(-__FLT_MAX__) << 32;
+    }
+    if (threadIdx.x < 2) ovf[threadIdx.x] = 0;
+    lds_barrier();
     if (mode == HHFM_MODE_FM) {
       for (int q2 = wv; q2 < kQPerWave; q2 += NW) {
         float x = l < k ? pq[q2][l] : 0.f;
         x = group_sum<kWave>(x);
         if (l == 0) cq_l[q2] = x;
       }
+      lds_barrier();
     }
   }
-  if (threadIdx.x < kQPerWave) cnt[threadIdx.x] = 0;
-  if (threadIdx.x == 0) again = 0;
-  __syncthreads();
-  HHFM_TMARK(1);
 
   // B operand (catalog_main): this lane's query j, k slices {EPC(2t+h) ..}
   float bq[KT][EPC];
@@ -351,371 +396,405 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       split3x8(x, qp[0][u], qp[1][u], qp[2][u]);
     }
   }
-  auto QP = [&](int pc, int u) -> bf16x8 { return qp[pc][u]; };
   const float cq = FM ? cq_l[j] : 0.f;
-
-  HHFM_TMARK(2);
-#if HHFM_FUSED_KO & 8   // knock-out: stop after the query phase (tile loads consumed)
-  {
-    float z = __uint_as_float(ar[0][0].x) + __uint_as_float(QP(0, 0)[0]);
-    if (z == 1234.5f) out_s[0] = z;
-    return;
-  }
+#if HHFM_FUSED_TIMING
+  HHFM_TMARK(tm1);
+  tacc[0] += tm1 - tm0;
 #endif
-  // ---- 1. scores of this wave's T tiles, kept in registers ----
-  float sc[T][16];
-#pragma unroll
-  for (int tt = 0; tt < T; ++tt) {
-    const int tile = tile0 + tt;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[tt][r] = kNegInf;
-    if (tile >= ntiles) continue;   // wave-uniform
-    uint4 (&ar_)[KT] = ar[tt % PD];
-    // PD < T: this slot is refilled with tile tt + PD chunk by chunk
-    const bool refill = PD < T && tt + PD < T;
-    const int nxt = tile + PD < ntiles ? tile + PD : ntiles - 1;
-    const char* nrow = E + (item_row_begin + item_of(nxt)) * ROWB + 16 * h;
-    f32x16 acc = {0};
-    const float wcur = wr[tt % PD];
-    if constexpr (HHFM_FUSED_KO & 4) {
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        acc[t] += __uint_as_float(ar_[t].x) * (float)QP(0, 0)[t & 7];
-        if (refill) ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
-      }
-    } else if constexpr (SPLIT && BF16) {
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        const bf16x8 ai = __builtin_bit_cast(bf16x8, ar_[t]);
-        if (refill) ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(2, t), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(1, t), acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(0, t), acc, 0, 0, 0);
-      }
-    } else if constexpr (SPLIT) {
-#pragma unroll
-      for (int u = 0; u < KT / 2; ++u) {
-        const float x[8] = {__uint_as_float(ar_[2 * u].x), __uint_as_float(ar_[2 * u].y),
-                            __uint_as_float(ar_[2 * u].z), __uint_as_float(ar_[2 * u].w),
-                            __uint_as_float(ar_[2 * u + 1].x), __uint_as_float(ar_[2 * u + 1].y),
-                            __uint_as_float(ar_[2 * u + 1].z), __uint_as_float(ar_[2 * u + 1].w)};
-        if (refill) ar_[2 * u] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u));
-        if (refill) ar_[2 * u + 1] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u + 1));
-        bf16x8 i0, i1, i2;
-        split3x8(x, i0, i1, i2);
-        const bf16x8 q0 = QP(0, u), q1 = QP(1, u), q2 = QP(2, u);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, q0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, q1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q2, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, q0, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q1, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, q0, acc, 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < KT; ++t) {
-        float av[EPC];
-        if constexpr (BF16) {
-          const uint32_t r4[4] = {ar_[t].x, ar_[t].y, ar_[t].z, ar_[t].w};
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            av[2 * v] = __uint_as_float(r4[v] << 16);
-            av[2 * v + 1] = __uint_as_float(r4[v] & 0xffff0000u);
-          }
-        } else {
-          av[0] = __uint_as_float(ar_[t].x); av[1] = __uint_as_float(ar_[t].y);
-          av[2] = __uint_as_float(ar_[t].z); av[3] = __uint_as_float(ar_[t].w);
-        }
-        if (refill) ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
-#pragma unroll
-        for (int e = 0; e < EPC; ++e)
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
-      }
-    }
-    if constexpr (FM) {   // D[i][j] += w_i·1 + 1·(q_j·f_j)   (catalog_main)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f, h == 0 ? 1.f : cq, acc,
-                                                 0, 0, 0);
-      if (refill) wr[tt % PD] = w ? w[item_row_begin + item_of(nxt)] : 0.f;
-    }
-    const int ibase = tile * kTile;
-    if (ibase + kTile <= N) {   // wave-uniform: only the catalog's last tile is partial
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc[tt][r] = acc[r];
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        sc[tt][r] = ibase + row < N ? acc[r] : kNegInf;
-      }
-    }
-    // one tile in flight: keeps the compiler from hoisting later tiles' loads
-    // (the unrolled loop otherwise holds every tile's A operand at once)
-    asm volatile("" ::: "memory");
-  }
 
-#if HHFM_FUSED_KO & 2
   {
-    float z = 0.f;
-#pragma unroll
-    for (int tt = 0; tt < T; ++tt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) z += sc[tt][r];
-    if (z == 1234.5f) out_s[0] = z;
-    return;
-  }
-#endif
-  HHFM_TMARK(3);
-  // ---- 2. threshold from the group maxima ----
-  float tmax[T];   // this lane's group maxima (also: tiles with nothing to pass)
-#pragma unroll
-  for (int tt = 0; tt < T; ++tt) {
-    float m = sc[tt][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) m = fmaxf(m, sc[tt][r]);
-    tmax[tt] = m;
-  }
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    float m = tmax[g * TG];
-#pragma unroll
-    for (int u = 1; u < TG; ++u) m = fmaxf(m, tmax[g * TG + u]);
-    gmax[j][(wv * 4 + g) * 2 + h] = m;
-  }
-  __syncthreads();
-  {   // this wave's kQPerWave / NW queries side by side (independent networks)
-    constexpr int QW = kQPerWave / NW;
-    float m[QW];
-#pragma unroll
-    for (int u = 0; u < QW; ++u) m[u] = l < NG ? gmax[wv + NW * u][l] : kNegInf;
-    sort_desc_scores_n<64, QW>(m);
-#pragma unroll
-    for (int u = 0; u < QW; ++u) {
-      const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m[u]), K - 1));
-      if (l == 0) {
-        thr_s[wv + NW * u] = t;
-        thr_i[wv + NW * u] = kNoIdx;   // every item scoring t passes
-      }
-    }
-  }
-  __syncthreads();
-
-#if HHFM_FUSED_KO & 1
-  {
-    float z = thr_s[j];
-#pragma unroll
-    for (int tt = 0; tt < T; ++tt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) z += sc[tt][r];
-    if (z == 1234.5f) out_s[0] = z;
-    return;
-  }
-#endif
-  HHFM_TMARK(4);
-  // ---- 3. survivors to the per-query lists (re-filtered on overflow) ----
-  for (;;) {
-    // queries past B (a zero vector: every HHFM score ties at 0) add nothing
-    const float ts = q0 + j < B ? thr_s[j] : __builtin_huge_valf();
-    const int32_t ti = q0 + j < B ? thr_i[j] : -1;
-    // item index of (tile tt, row r) = ib + 32 tt + row(r); laundered so the
-    // compiler does not hoist 16 T indices out of the loop into registers
-    int32_t ib = tile0 * kTile + 4 * h;
-    asm volatile("" : "+v"(ib));
-    uint32_t pm[T];   // pass bits of the lane's 16 rows per tile
-    int n = 0;
-    // the first round (t finite, ti = kNoIdx on every lane) is `score >= t`
-    // (items past N hold -inf); a raised pair threshold takes the full test
-    if (__ballot(ti != kNoIdx || !(ts > kNegInf)) == 0) {
-#pragma unroll
-      for (int tt = 0; tt < T; ++tt) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) m |= sc[tt][r] >= ts ? 1u << r : 0u;
-        pm[tt] = m;
-      }
-    } else {
-#pragma unroll
-      for (int tt = 0; tt < T; ++tt) {
-        uint32_t m = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int32_t it = ib + tt * kTile + (r & 3) + 8 * (r >> 2);
-          const float x = sc[tt][r];
-          const bool pass = (it < N) & ((x > ts) | ((x == ts) & (it <= ti)));
-          m |= pass ? 1u << r : 0u;
-        }
-        pm[tt] = m;
-      }
-    }
-#pragma unroll
-    for (int tt = 0; tt < T; ++tt) n += __popc(pm[tt]);
-    HHFM_TMARK(7);
-    int pos = n ? atomicAdd(&cnt[j], n) : 0;
-    HHFM_TMARK(8);
-    asm volatile("" : "+v"(ib));   // recompute the indices below (no 16 T live values)
-    // (score, index) as one 8-B slot; slots past the list's end go to the
-    // query's spare slot kFusedCap
-    constexpr int kQS = kFusedCap + 1;   // slots per query (the last: spare)
-    const int qbase = j * kQS;
+    HHFM_TMARK(tm0);
+    // ---- 1. scores of this wave's T tiles, kept in registers ----
+    float sc[T][16];
 #pragma unroll
     for (int tt = 0; tt < T; ++tt) {
-      const uint32_t m = pm[tt];
-      if (__ballot(m != 0) != 0) {
-        // only the passing rows write (exec-masked stores; branch-free
-        // writes of every row to a dummy slot measured 2 % slower)
+      const int tile = tile0 + tt;
+      uint4 (&ar_)[KT] = ar[tt % PD];
+      // this slot is refilled with tile tt + PD, chunk by chunk
+      const int nxt = tile_of(tt + PD);
+      const char* nrow = E + (item_row_begin + item_of(nxt)) * ROWB + 16 * h;
+      f32x16 acc = {0};
+      const float wcur = wr[tt % PD];
+      if constexpr (SPLIT && BF16) {
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const bf16x8 ai = __builtin_bit_cast(bf16x8, ar_[t]);
+          ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[2][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[1][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[0][t], acc, 0, 0, 0);
+        }
+      } else if constexpr (SPLIT) {
+#pragma unroll
+        for (int u = 0; u < KT / 2; ++u) {
+          const float x[8] = {__uint_as_float(ar_[2 * u].x), __uint_as_float(ar_[2 * u].y),
+                              __uint_as_float(ar_[2 * u].z), __uint_as_float(ar_[2 * u].w),
+                              __uint_as_float(ar_[2 * u + 1].x), __uint_as_float(ar_[2 * u + 1].y),
+                              __uint_as_float(ar_[2 * u + 1].z), __uint_as_float(ar_[2 * u + 1].w)};
+          ar_[2 * u] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u));
+          ar_[2 * u + 1] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u + 1));
+          bf16x8 i0, i1, i2;
+          split3x8(x, i0, i1, i2);
+          const bf16x8 p0 = qp[0][u], p1 = qp[1][u], p2 = qp[2][u];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, p0, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, p1, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, p2, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, p0, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, p1, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, p0, acc, 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          float av[EPC];
+          if constexpr (BF16) {
+            const uint32_t r4[4] = {ar_[t].x, ar_[t].y, ar_[t].z, ar_[t].w};
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              av[2 * v] = __uint_as_float(r4[v] << 16);
+              av[2 * v + 1] = __uint_as_float(r4[v] & 0xffff0000u);
+            }
+          } else {
+            av[0] = __uint_as_float(ar_[t].x); av[1] = __uint_as_float(ar_[t].y);
+            av[2] = __uint_as_float(ar_[t].z); av[3] = __uint_as_float(ar_[t].w);
+          }
+          ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
+#pragma unroll
+          for (int e = 0; e < EPC; ++e)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], bq[t][e], acc, 0, 0, 0);
+        }
+      }
+      if constexpr (FM) {   // D[i][j] += w_i·1 + 1·(q_j·f_j)   (catalog_main)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h == 0 ? wcur : 1.f, h == 0 ? 1.f : cq, acc,
+                                                   0, 0, 0);
+        wr[tt % PD] = w ? w[item_row_begin + item_of(nxt)] : 0.f;
+      }
+      const int ibase = tile * kTile;
+      if (ibase + kTile <= N) {   // wave-uniform: only the catalog's last tiles are partial
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[tt][r] = acc[r];
+      } else {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const bool pb = (m >> r) & 1u;
-          if (pb)
-            cbuf[qbase + min(pos, kFusedCap)] =
-                make_float2(sc[tt][r], __int_as_float(ib + tt * kTile + (r & 3) + 8 * (r >> 2)));
-          pos += pb ? 1 : 0;
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+          sc[tt][r] = ibase + row < N ? acc[r] : kNegInf;
         }
       }
-      // one tile's slots at a time (the compiler otherwise forms all 16 T
-      // slot addresses up front)
-      asm volatile("" : "+v"(pos) : : "memory");
+      // one tile in flight: keeps the compiler from hoisting later tiles' loads
+      asm volatile("" ::: "memory");
     }
-    HHFM_TMARK(9);
-    // a lane whose last slot lies past the cap flags the overflow: the
-    // common case (no list overflowed) then costs one barrier
-    if (pos > kFusedCap) again = 1;
-    __syncthreads();
-    HHFM_TMARK(10);
-    if (!again) break;
-    // overflowed queries: the K-th best pair among the kFusedCap collected
-    // becomes the threshold (at least K items reach it), and the range is
-    // filtered again from an empty list
-    for (int qq = wv; qq < kQPerWave; qq += NW) {
-      if (cnt[qq] <= kFusedCap) continue;   // wave-uniform
-      const float2 e0 = cbuf[qq * (kFusedCap + 1) + l], e1 = cbuf[qq * (kFusedCap + 1) + l + 64];
-      float s0 = e0.x, s1 = e1.x;
-      int32_t i0 = __float_as_int(e0.y), i1 = __float_as_int(e1.y);
-      bitonic_sort_desc<64>(s0, i0);
-      bitonic_sort_desc<64>(s1, i1);
-      merge_lists<64>(s0, i0, s1, i1);   // the best 64 of the 128, sorted
-      const float ns = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s0), K - 1));
-      const int32_t ni = __builtin_amdgcn_readlane(i0, K - 1);
-      if (l == 0) {
-        thr_s[qq] = ns;
-        thr_i[qq] = ni;
-        cnt[qq] = -1;   // marks: filter this query again
+#if HHFM_FUSED_TIMING
+    HHFM_TMARK(tm1);
+    tacc[1] += tm1 - tm0;
+    tm0 = tm1;
+#endif
+
+    // ---- 2. threshold: K-th largest of the 32 offered tile maxima ----
+    {
+      float mr[R];   // this lane's R largest tile maxima, descending
+#pragma unroll
+      for (int r = 0; r < R; ++r) mr[r] = kNegInf;
+#pragma unroll
+      for (int tt = 0; tt < T; ++tt) {
+        float m = sc[tt][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) m = fmaxf(m, sc[tt][r]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {   // insert: the larger stays, the smaller moves on
+          const float hi = fmaxf(mr[r], m);
+          m = fminf(mr[r], m);
+          mr[r] = hi;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) gmx[j][(wv * 2 + h) * R + r] = mr[r];
+    }
+    lds_barrier();
+    {   // wave wv: queries QW wv + 2u + h, one per 32-lane half
+      constexpr int QW = kQPerWave / NW, U = QW / 2;
+      float m[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) m[u] = gmx[wv * QW + 2 * u + h][j];
+      sort_desc_scores_n<32, U>(m);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float t = shfl_f(m[u], (h << 5) + K - 1);
+        const int qq = wv * QW + 2 * u + h;
+        // a raised pair threshold of equal score stays (its key is larger)
+        const uint64_t tk = (uint64_t)ukey(t) << 32;
+        if (j == 0 && tk > thr_k[qq]) thr_k[qq] = tk;
       }
     }
-    __syncthreads();
-    // queries not overflowed keep their lists: their lanes add nothing
-    const bool redo = cnt[j] < 0;
-    __syncthreads();
-    if (threadIdx.x == 0) again = 0;
-    if (threadIdx.x < kQPerWave && cnt[threadIdx.x] < 0) cnt[threadIdx.x] = 0;
-    if (!redo) {
-      thr_s[j] = __builtin_huge_valf();   // (written by both lanes of j: same value)
-      thr_i[j] = -1;
+    if (threadIdx.x < kQPerWave) cprev[threadIdx.x] = cnt[threadIdx.x];
+    lds_barrier();
+#if HHFM_FUSED_TIMING
+    HHFM_TMARK(tm1);
+    tacc[2] += tm1 - tm0;
+    tm0 = tm1;
+#endif
+
+    // ---- 3. survivors to the per-query lists (re-filtered on overflow) ----
+    const int qbase = j * kQS;
+    bool first = true;
+#pragma unroll 1
+    for (;;) {
+      // this round's filter: every live query in the chunk's first round,
+      // afterwards only the queries whose list overflowed (redo); rows past B
+      // never pass (their zero query ties every item at 0)
+      const bool mine = live && (first || redo[j]);
+      const uint64_t tk = thr_k[j];
+      const uint32_t tlo = (uint32_t)tk;
+      // NaN: no score passes
+      const float ts = mine ? ukey_inv((uint32_t)(tk >> 32)) : __builtin_nanf("");
+      // item index of (tile tt, row r) = ib + 32 tt + row(r); laundered so the
+      // compiler does not hoist 16 T indices out of the loop into registers
+      int32_t ib = tile0 * kTile + 4 * h;
+      asm volatile("" : "+v"(ib));
+      uint32_t pm[T];   // pass bits of the lane's 16 rows per tile
+      // a score threshold (low word 0 on every lane) is `score >= t` (items
+      // past N hold -inf); a raised pair threshold takes the key test
+      if (__ballot(mine && tlo != 0) == 0) {
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int r = 15; r >= 0; --r) m = m + m + (sc[tt][r] >= ts ? 1u : 0u);
+          pm[tt] = m;
+        }
+      } else {
+        // key >= (ukey(ts), ~ti)  <=>  x > ts, or x == ts and index <= ti
+        const int32_t ti = ~(int32_t)tlo;
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+          uint32_t m = 0;
+#pragma unroll
+          for (int r = 15; r >= 0; --r) {
+            const int32_t it = ib + tt * kTile + (r & 3) + 8 * (r >> 2);
+            const float x = sc[tt][r];
+            const bool pass = (it < N) & ((x > ts) | ((x == ts) & (it <= ti)));
+            m = m + m + (pass ? 1u : 0u);
+          }
+          pm[tt] = m;
+        }
+      }
+      int n = 0;
+#pragma unroll
+      for (int tt = 0; tt < T; ++tt) n += __popc(pm[tt]);
+      int pos = atomicAdd(&cnt[j], n);
+      asm volatile("" : "+v"(ib));   // recompute the indices below (no 16 T live values)
+      // one survivor per lane per step (lowest row first); a lane without one
+      // writes the query's spare slot (no exec-mask branches)
+#pragma unroll
+      for (int tt = 0; tt < T; ++tt) {
+        uint32_t m = pm[tt];
+#pragma unroll 1
+        while (__ballot(m != 0) != 0) {
+          const int r = __builtin_ctz(m | 0x10000u) & 15;
+          const float x = select16(sc[tt], r);
+          const int32_t it = ib + tt * kTile + (r & 3) + 8 * (r >> 2);
+          const int slot = m ? (pos < kFusedCap ? pos : kFusedCap) : kFusedCap;
+          cbuf[qbase + slot] = ekey(x, it);
+          pos += m ? 1 : 0;
+          m &= m - 1;
+        }
+      }
+      // a lane whose last slot lies past the cap flags the overflow in this
+      // round's flag word (two words alternate, so the reset of the next
+      // round's word never races with this round's writers)
+      if (pos > kFusedCap) ovf[rnd & 1] = 1;
+      lds_barrier();
+      const bool over = ovf[rnd & 1] != 0;
+      if (threadIdx.x == 0) ovf[(rnd + 1) & 1] = 0;   // last read before this barrier
+      ++rnd;
+      first = false;
+      if (!over) break;
+      // overflowed queries (rare: heavy exact ties): the K-th best key among
+      // the kFusedCap collected becomes the threshold (at least K items reach
+      // it; only K of the collected do), the earlier chunks' entries [0,
+      // cprev) below it are dropped, and the chunk is filtered again for
+      // those queries only
+#pragma unroll 1
+      for (int qq = wv; qq < kQPerWave; qq += NW) {
+        const bool of = cnt[qq] > kFusedCap;   // wave-uniform
+        if (l == 0) redo[qq] = of ? 1 : 0;
+        if (!of) continue;
+        const uint64_t e0 = cbuf[qq * kQS + l], e1 = cbuf[qq * kQS + l + 64];
+        uint64_t k0 = e0, k1 = e1;
+        sort_keys_desc<64>(k0);
+        sort_keys_desc<64>(k1);
+        merge_keys<64>(k0, k1);   // the best 64 of the 128, sorted
+        const uint32_t nlo = __builtin_amdgcn_readlane((int32_t)(uint32_t)k0, K - 1);
+        const uint32_t nhi = __builtin_amdgcn_readlane((int32_t)(uint32_t)(k0 >> 32), K - 1);
+        const uint64_t nk = ((uint64_t)nhi << 32) | nlo;
+        const int np = cprev[qq];
+        const bool a0 = l < np && e0 >= nk;
+        const bool a1 = l + 64 < np && e1 >= nk;
+        const uint64_t b0 = __ballot(a0), b1 = __ballot(a1);
+        const int p0 = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u));
+        const int p1 = __popcll(b0) + (int)__builtin_amdgcn_mbcnt_hi(
+                                          (uint32_t)(b1 >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+        __builtin_amdgcn_wave_barrier();   // every lane's reads before any write
+        if (a0) cbuf[qq * kQS + p0] = e0;
+        if (a1) cbuf[qq * kQS + p1] = e1;
+        if (l == 0) {
+          const int kept = __popcll(b0) + __popcll(b1);
+          thr_k[qq] = nk;
+          cnt[qq] = kept;
+          cprev[qq] = kept;
+        }
+      }
+      lds_barrier();
     }
-    __syncthreads();
+#if HHFM_FUSED_TIMING
+    HHFM_TMARK(tm1);
+    tacc[3] += tm1 - tm0;
+#endif
   }
 
-  HHFM_TMARK(5);
-  // ---- 4. sort the survivors, write the top K ----
-  const int64_t ob = split * ostride_s;
-  {
-    // this wave's query pairs p = wv + NW u: each query in a 32-lane half;
-    // when every pair's lists fit 32 lanes (the common case: ~24 survivors)
-    // the pairs' networks run side by side
-    constexpr int PW = kQPerWave / 2 / NW;
-    bool small = true;
-#pragma unroll
-    for (int u = 0; u < PW; ++u) {
-      const int pp = wv + NW * u;
-      small = small && cnt[2 * pp] <= 32 && cnt[2 * pp + 1] <= 32;
-    }
-    if (small) {
-      float sv[PW];
-      int32_t iv[PW];
-#pragma unroll
-      for (int u = 0; u < PW; ++u) {
-        const int qq = 2 * (wv + NW * u) + h, nq = cnt[qq];
-        const float2 e = cbuf[qq * (kFusedCap + 1) + (j < nq ? j : 0)];
-        sv[u] = j < nq ? e.x : kNegInf;
-        iv[u] = j < nq ? __float_as_int(e.y) : kNoIdx;
-      }
-      bitonic_sort_desc_n<32, PW>(sv, iv);
-#pragma unroll
-      for (int u = 0; u < PW; ++u) {
-        const int qq = 2 * (wv + NW * u) + h;
-        const int64_t b = q0 + qq;
-        if (b < B && j < K) {
-          out_s[b * ostride_b + ob + j] = sv[u];
-          out_i[b * ostride_b + ob + j] = iv[u] == kNoIdx ? kNoIdx : iv[u] + gbase;
-        }
+  // ---- 4. per query: the range's entries at or above the final threshold,
+  // sorted (its exact top K) ----
+  // Two queries per pass, one per 32-lane half: a half's lanes load its
+  // query's entries 32 at a time, the passing ones are compacted into the
+  // wave's LDS scratch and one 32-lane key network sorts them (typically
+  // ~K·1.2 pass).  A query with more than 32 passing takes the 64-lane
+  // network (+ merges past 64), one query at a time.
+  HHFM_TMARK(tm0);
+  typedef __attribute__((address_space(1))) uint64_t gu64;
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  // rank r of query qq: the output (S = 1) or the range's list, stored
+  // write-through (sc1) for the merging workgroup
+  auto emit = [&](int qq, int r, uint64_t key) {
+    if (S == 1) {
+      const int64_t b = q0 + qq;
+      if (b < B && r < K) {
+        out_s[b * K + r] = ukey_inv((uint32_t)(key >> 32));
+        const int32_t it = ~(int32_t)(uint32_t)key;
+        out_i[b * K + r] = it == kNoIdx ? kNoIdx : it + gbase;
       }
     } else {
+      gu64* dst = (gu64*)(part + (((int64_t)blockIdx.x * kQPerWave + qq) << 5) + r);
+      __hip_atomic_store(dst, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+  {
+    constexpr int QW = kQPerWave / NW, U = QW / 2;
 #pragma unroll 1
-      for (int qi = 0; qi < 2 * PW; ++qi) {
-        const int qq = 2 * (wv + NW * (qi >> 1)) + (qi & 1), nq = cnt[qq];
-        // per pair: a pair whose lists both fit 32 lanes takes the 32-lane
-        // network (its second query is done with the first); a list of at
-        // most 64 one 64-lane sort
-        const int qo = qq ^ 1, no = cnt[qo];
-        if (nq <= 32 && no <= 32) {
-          if (qi & 1) continue;   // done with its pair
-          const int qh = qq + h, nh = h ? no : nq;
-          const float2 e = cbuf[qh * (kFusedCap + 1) + (j < nh ? j : 0)];
-          float sv[1] = {j < nh ? e.x : kNegInf};
-          int32_t iv[1] = {j < nh ? __float_as_int(e.y) : kNoIdx};
-          bitonic_sort_desc_n<32, 1>(sv, iv);
-          const int64_t b = q0 + qh;
-          if (b < B && j < K) {
-            out_s[b * ostride_b + ob + j] = sv[0];
-            out_i[b * ostride_b + ob + j] = iv[0] == kNoIdx ? kNoIdx : iv[0] + gbase;
-          }
-          continue;
-        }
-        if (nq <= 64) {
-          const float2 e = cbuf[qq * (kFusedCap + 1) + (l < nq ? l : 0)];
-          float s1 = l < nq ? e.x : kNegInf;
-          int32_t i1 = l < nq ? __float_as_int(e.y) : kNoIdx;
-          bitonic_sort_desc<64>(s1, i1);
-          const int64_t b = q0 + qq;
-          if (b < B && l < K) {
-            out_s[b * ostride_b + ob + l] = s1;
-            out_i[b * ostride_b + ob + l] = i1 == kNoIdx ? kNoIdx : i1 + gbase;
-          }
-          continue;
-        }
-        float ls = kNegInf;
-        int32_t li = kNoIdx;
+    for (int u = 0; u < U; ++u) {
+      const int qq = wv * QW + 2 * u + h;
+      const int nq = cnt[qq] < kFusedCap ? cnt[qq] : kFusedCap;
+      const uint64_t tk = thr_k[qq];
+      int nv = 0;   // passing entries of this half's query so far
 #pragma unroll 1
-        for (int c = 0; c < nq; c += 64) {
-          const float2 e = cbuf[qq * (kFusedCap + 1) + (c + l < nq ? c + l : 0)];
-          float s = c + l < nq ? e.x : kNegInf;
-          int32_t i = c + l < nq ? __float_as_int(e.y) : kNoIdx;
-          bitonic_sort_desc<64>(s, i);
-          merge_lists<32>(ls, li, s, i);
-          if (l >= 32) {
-            ls = kNegInf;
-            li = kNoIdx;
+      for (int c = 0; c < kFusedCap; c += 32) {
+        if (__ballot(c < nq) == 0) break;   // both halves done
+        const uint64_t e = cbuf[qq * kQS + (c + j < nq ? c + j : kFusedCap)];
+        const bool ok = c + j < nq && e >= tk;
+        const uint64_t bm = __ballot(ok);
+        const uint32_t hm = h ? (uint32_t)(bm >> 32) : (uint32_t)bm;
+        const int pre = __popc(hm & ((1u << j) - 1u));
+        if (ok && nv + pre < 32) fscr[wv][(h << 5) + nv + pre] = e;
+        nv += __popc(hm);
+      }
+      if (__ballot(nv > 32) == 0) {
+        uint64_t key = j < nv ? fscr[wv][(h << 5) + j] : 0ull;
+        sort_keys_desc<32>(key);
+        emit(qq, j, key);
+      } else {   // rare: one query at a time over the whole wave
+#pragma unroll 1
+        for (int hh = 0; hh < 2; ++hh) {
+          const int q2 = wv * QW + 2 * u + hh;
+          const int n2 = cnt[q2] < kFusedCap ? cnt[q2] : kFusedCap;
+          const uint64_t t2 = thr_k[q2];
+          uint64_t top = 0;
+#pragma unroll 1
+          for (int c = 0; c < n2; c += kWave) {
+            const uint64_t e = cbuf[q2 * kQS + (c + l < n2 ? c + l : kFusedCap)];
+            uint64_t key = (c + l < n2 && e >= t2) ? e : 0ull;
+            sort_keys_desc<64>(key);
+            if (c == 0) top = key;
+            else merge_keys<32>(top, key);
+            if (l >= 32) top = 0;
           }
-        }
-        const int64_t b = q0 + qq;
-        if (b < B && l < K) {
-          out_s[b * ostride_b + ob + l] = ls;
-          out_i[b * ostride_b + ob + l] = li == kNoIdx ? kNoIdx : li + gbase;
+          if (l < 32) emit(q2, l, top);
         }
       }
     }
   }
 #if HHFM_FUSED_TIMING
-  HHFM_TMARK(6);
+  HHFM_TMARK(tm1);
+  tacc[4] += tm1 - tm0;
+  tm0 = tm1;
+#endif
+
+  // ---- 5. S > 1: hand-off, the last arriving workgroup merges ----
+  bool merged = false;
+  if (S > 1) {
+    // every storing wave drains its sc1 stores, then the barrier, then ONE
+    // lane's agent-scope add for the whole workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if (threadIdx.x == 0) {
+      const uint32_t old = __hip_atomic_fetch_add((gu32*)(arrive + g), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+      last_sh = old == (uint32_t)(S - 1);
+    }
+    lds_barrier();
+    merged = last_sh != 0;   // uniform
+    if (merged) {
+      // no instruction: keeps the sc1 loads below the barrier
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr int QW = kQPerWave / NW;
+      constexpr int kMaxS = kFusedMaxS;
+#pragma unroll 1
+      for (int u = 0; u < QW; ++u) {
+        const int qq = wv * QW + u;
+        // lane (h, j) holds rank j of the lists h, h + 2, ...: all loads in
+        // flight before the merges
+        uint64_t v[kMaxS / 2];
+#pragma unroll
+        for (int x = 0; x < kMaxS / 2; ++x) {
+          const int sl = 2 * x + h;
+          v[x] = 0;
+          if (2 * x < S) {   // wave-uniform
+            const gu64* src =
+                (const gu64*)(part + ((((int64_t)g * S + (sl < S ? sl : 0)) * kQPerWave + qq) << 5) + j);
+            const uint64_t t = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[x] = sl < S ? t : 0ull;
+          }
+        }
+        uint64_t a = v[0];
+#pragma unroll
+        for (int x = 1; x < kMaxS / 2; ++x)
+          if (2 * x < S) merge_keys<32>(a, v[x]);
+        merge_keys<32>(a, xor_lane64(a, 32));   // the odd lists' half into the even's
+        const int64_t b = q0 + qq;
+        if (b < B && l < K) {
+          out_s[b * K + l] = ukey_inv((uint32_t)(a >> 32));
+          const int32_t it = ~(int32_t)(uint32_t)a;
+          out_i[b * K + l] = it == kNoIdx ? kNoIdx : it + gbase;
+        }
+      }
+      // re-arm the counter for the next call (stream order publishes it)
+      if (threadIdx.x == 0)
+        __hip_atomic_store((gu32*)(arrive + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#if HHFM_FUSED_TIMING
+  HHFM_TMARK(tm1);
+  tacc[5] += tm1 - tm0;
   if (l == 0) {
-    atomicAdd(&g_fused_t[0], tmk[1] - tmk[0]);
-    atomicAdd(&g_fused_t[1], tmk[2] - tmk[1]);
-    atomicAdd(&g_fused_t[2], tmk[3] - tmk[2]);
-    atomicAdd(&g_fused_t[3], tmk[4] - tmk[3]);
-    atomicAdd(&g_fused_t[4], tmk[5] - tmk[4]);
-    atomicAdd(&g_fused_t[5], tmk[6] - tmk[5]);
-    atomicAdd(&g_fused_t[6], 1ull);
+#pragma unroll
+    for (int p = 0; p < 5; ++p) atomicAdd(&g_fused_t[p], tacc[p]);
+    atomicAdd(&g_fused_t[5], 1ull);
+    if (merged) {
+      atomicAdd(&g_fused_t[6], 1ull);
+      atomicAdd(&g_fused_t[7], tacc[5]);
+    }
   }
 #endif
+  (void)merged;
 }
 
 }  // namespace hhfm

@@ -988,9 +988,9 @@ struct Plan {
   bool dense;            // small catalog: score matrix + dense top-K
   int64_t ldsc;
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
-  int fS, fT;            // fused small-catalog kernel: workgroups per 32 queries, tiles per wave
   int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
   int sS[2], stps[2];            // the same over the seed's items (its GMAX pass)
+  int fS;                // fused small-catalog kernel: workgroups (item ranges) per 32 queries
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
       off_seed_i, total;
 };
@@ -1049,7 +1049,9 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
     ring_splits(p.rnqb[v], v, ntiles, p.rS[v], p.rtps[v]);
   }
   const int nsplit = std::max(p.S, std::max(p.rS[0], p.rS[1]));
-  size_t off = 0;
+  // [0, HHFM_CATALOG_WS_ZERO): the fused kernel's arrival counters, zero
+  // before the first call and re-armed by every call; no plan writes there
+  size_t off = HHFM_CATALOG_WS_ZERO;
   p.off_H = off;   off += align256((size_t)p.Bpad * k * sizeof(float));
   p.off_cst = off; off += align256((size_t)p.Bpad * sizeof(float));
   p.off_thr = off; off += align256((size_t)p.Bpad * sizeof(int32_t));
@@ -1061,25 +1063,18 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
   } else {
     p.off_pi = off;
   }
-  // the fused small-catalog kernel (catalog_fused.h): S_f workgroups per
-  // 32 queries, each kFusedWaves waves x T tiles; S_f > 1 merges lists of K
-  // from off_ps.  (8 tiles per wave — half the workgroups, one round on the
-  // CUs at 3,000 queries — ran 4 % faster at C3 but spills 150 B of
-  // registers per lane: not kept, profiles/r05_c3_fused.txt)
-  {
-    const int fS4 = (ntiles + kFusedWaves * kFusedTiles - 1) / (kFusedWaves * kFusedTiles);
-    p.fT = kFusedTiles;
-    p.fS = fS4;
-    if (p.dense && fS4 > 1 && nsplit < fS4) {
-      off = p.off_ps;
-      off += align256((size_t)B * fS4 * K * sizeof(float));
-      p.off_pi = off;
-      off += align256((size_t)B * fS4 * K * sizeof(int32_t));
-    }
-  }
   p.ldsc = (N + 3) & ~3;
   p.off_sc = off;
-  if (p.dense) off += align256((size_t)B * p.ldsc * sizeof(float));
+  // the fused kernel's range lists [groups][S][32 queries][32] keys share the
+  // score matrix's region (never both in one call)
+  p.fS = (ntiles + kFusedWaves * kFusedTiles - 1) / (kFusedWaves * kFusedTiles);
+  if (p.dense) {
+    const size_t sc_bytes = (size_t)B * p.ldsc * sizeof(float);
+    const size_t fl_bytes = p.fS > 1 ? (size_t)((B + kQPerWave - 1) / kQPerWave) * p.fS *
+                                           kQPerWave * 32 * sizeof(uint64_t)
+                                     : 0;
+    off += align256(sc_bytes > fl_bytes ? sc_bytes : fl_bytes);
+  }
   // seed: up to kSeedMax items, kSeedBudget query-item pairs and 1/16 of the
   // catalog (the seed pass then costs <= ~6 % of the MFMA work); none below
   // 4,096 items (catalogs under 65,536 items)
@@ -1232,44 +1227,36 @@ static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const fl
                        ldsc, 0, 0, gthr);
 }
 
-template <bool BF16, int KT, bool FM, int T>
-static void launch_fused_t(int64_t B, int nqb, int S, const int32_t* qidx, int ncols, int mode,
-                         int ucol, int c0, int c1, int t0, int t1, const char* E, int64_t M,
-                         int64_t irb, int32_t N, const float* w, int K, float* os, int32_t* oi,
-                         int64_t sb, int64_t ss, int32_t gbase, int32_t plan, hipStream_t st) {
+// the fused small-catalog kernel (catalog_fused.h): S 8-wave workgroups per
+// 32 queries, each over one range of 8 x kFusedTiles item tiles; the last to
+// finish merges the S range lists
+template <bool BF16, int KT, bool FM>
+static void launch_fused(int64_t B, int S, const int32_t* qidx, int ncols, int mode, int ucol,
+                         int c0, int c1, int t0, int t1, const char* E, int64_t M, int64_t irb,
+                         int32_t N, const float* w, int K, float* os, int32_t* oi, int32_t gbase,
+                         uint32_t* arrive, uint64_t* part, int32_t plan, hipStream_t st) {
   constexpr bool kCanSplit = BF16 || KT >= 2;
+  constexpr int T = kFusedTiles;
+  const int nqb = (int)((B + kQPerWave - 1) / kQPerWave);
   if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
     hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, kCanSplit, T>), dim3(nqb * S),
-                       dim3(kFusedWaves * 64), 0, st,
-                       qidx, B, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, S, os, oi,
-                       sb, ss, gbase);
+                       dim3(kFusedWaves * 64), 0, st, qidx, B, ncols, mode, ucol, c0, c1, t0, t1,
+                       E, M, irb, N, w, K, os, oi, gbase, S, arrive, part);
   else
     hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, false, T>), dim3(nqb * S),
-                       dim3(kFusedWaves * 64), 0, st,
-                       qidx, B, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, S, os, oi,
-                       sb, ss, gbase);
-}
-
-template <bool BF16, int KT, bool FM>
-static void launch_fused(int T, int64_t B, int nqb, int S, const int32_t* qidx, int ncols,
-                         int mode, int ucol, int c0, int c1, int t0, int t1, const char* E,
-                         int64_t M, int64_t irb, int32_t N, const float* w, int K, float* os,
-                         int32_t* oi, int64_t sb, int64_t ss, int32_t gbase, int32_t plan,
-                         hipStream_t st) {
-  (void)T;
-  launch_fused_t<BF16, KT, FM, kFusedTiles>(B, nqb, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E,
-                                            M, irb, N, w, K, os, oi, sb, ss, gbase, plan, st);
+                       dim3(kFusedWaves * 64), 0, st, qidx, B, ncols, mode, ucol, c0, c1, t0, t1,
+                       E, M, irb, N, w, K, os, oi, gbase, S, arrive, part);
 }
 
 template <bool BF16, bool FM>
-static bool dispatch_fused(int KT, int T, int64_t B, int nqb, int S, const int32_t* qidx, int ncols,
-                           int mode, int ucol, int c0, int c1, int t0, int t1, const char* E,
-                           int64_t M, int64_t irb, int32_t N, const float* w, int K, float* os,
-                           int32_t* oi, int64_t sb, int64_t ss, int32_t gbase, int32_t plan,
+static bool dispatch_fused(int KT, int64_t B, int S, const int32_t* qidx, int ncols, int mode,
+                           int ucol, int c0, int c1, int t0, int t1, const char* E, int64_t M,
+                           int64_t irb, int32_t N, const float* w, int K, float* os, int32_t* oi,
+                           int32_t gbase, uint32_t* arrive, uint64_t* part, int32_t plan,
                            hipStream_t st) {
 #define HHFM_FUSED(KT_) \
-  launch_fused<BF16, KT_, FM>(T, B, nqb, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, \
-                              w, K, os, oi, sb, ss, gbase, plan, st)
+  launch_fused<BF16, KT_, FM>(B, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, \
+                              os, oi, gbase, arrive, part, plan, st)
   switch (KT) {
     case 1: HHFM_FUSED(1); break;
     case 2: HHFM_FUSED(2); break;
@@ -1419,35 +1406,28 @@ extern "C" int hhfm_catalog_topk_ex(
     if (rc != HHFM_OK) return rc;
   }
 
-  // small catalogs: scores and top-K in one kernel (catalog_fused.h) for
-  // >= 1,024 queries; fewer run latency-bound on few CUs, where the score
-  // matrix path measured faster (300 queries: 22.4 vs 24.8 us of kernel
-  // time; 3,000: 46.1 vs 44.0, profiles/r05_c3_paths.txt).  HHFM_PLAN_STORE
-  // forces the matrix path, HHFM_PLAN_FUSED the fused kernel at any size.
-  const bool fused_size = B >= 1024 || (plan & HHFM_PLAN_FUSED);
-  if (p.dense && fused_size && K <= 32 && KT <= 8 &&
+  // small catalogs: scores and top-K in one kernel launch (catalog_fused.h):
+  // the default up to 8,192 items (one workgroup walks the whole catalog for
+  // its 32 queries); HHFM_PLAN_STORE forces the score-matrix path,
+  // HHFM_PLAN_FUSED the fused kernel up to the dense limit
+  const bool fused_size = item_count <= 8192 || (plan & HHFM_PLAN_FUSED);
+  if (p.dense && fused_size && K <= 32 && KT <= 8 && p.fS <= kFusedMaxS &&
+      (B + kQPerWave - 1) / kQPerWave <= kFusedMaxGroups &&
       ctx_end - ctx_begin <= kFusedMaxCtx && time_end - time_begin <= kFusedMaxCtx &&
       !(plan & (HHFM_PLAN_GEMM | HHFM_PLAN_STORE))) {
     const bool fmm = mode == HHFM_MODE_FM;
     const float* wv = (fmm && w) ? w : nullptr;
-    float* os = p.fS > 1 ? reinterpret_cast<float*>(ws + p.off_ps) : top_score;
-    int32_t* oi = p.fS > 1 ? reinterpret_cast<int32_t*>(ws + p.off_pi) : top_idx;
-    const int64_t sb = (int64_t)p.fS * K, ss = p.fS > 1 ? K : 0;
-    const int32_t gb = global_item_base;   // order-preserving shift
-    const int nqb32 = (int)((B + kQPerWave - 1) / kQPerWave);
-#define HHFM_FARGS KT, p.fT, B, nqb32, p.fS, qidx, ncols, mode, user_col, ctx_begin, ctx_end, \
-    time_begin, time_end, Eb, features_M, (int64_t)item_row_begin, item_count, wv, K, os, oi, \
-    sb, ss, gb, plan, st
+    uint32_t* arrive = reinterpret_cast<uint32_t*>(ws);
+    uint64_t* part = reinterpret_cast<uint64_t*>(ws + p.off_sc);
+#define HHFM_FARGS KT, B, p.fS, qidx, ncols, mode, user_col, ctx_begin, ctx_end, time_begin, \
+    time_end, Eb, features_M, (int64_t)item_row_begin, item_count, wv, K, top_score, top_idx, \
+    global_item_base, arrive, part, plan, st
     const bool ok = bf16 ? (fmm ? dispatch_fused<true, true>(HHFM_FARGS)
                                 : dispatch_fused<true, false>(HHFM_FARGS))
                          : (fmm ? dispatch_fused<false, true>(HHFM_FARGS)
                                 : dispatch_fused<false, false>(HHFM_FARGS));
 #undef HHFM_FARGS
-    if (ok) {
-      if (p.fS > 1)
-        launch_merge(os, oi, p.fS, B, K, /*stride_r=*/K, /*stride_b=*/sb, top_score, top_idx, st);
-      return (int)hipGetLastError();
-    }
+    if (ok) return (int)hipGetLastError();
   }
 
   {

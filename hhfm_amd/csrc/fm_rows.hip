@@ -31,6 +31,15 @@ namespace hhfm {
 #ifndef HHFM_K1_WMAP
 #define HHFM_K1_WMAP 0
 #endif
+// diagnostic (timing only, wrong results; default 0): 1 — fields 2.. (the
+// context columns at configs[1]) keep their ids and `w` gathers but their
+// embedding rows are not loaded (zeros); scripts/diag/k1_ctx_ko.sh
+#ifndef HHFM_K1_CTXKO
+#define HHFM_K1_CTXKO 0
+#endif
+#if (HHFM_K1_WMAP || HHFM_K1_CTXKO) && !defined(HHFM_DIAG_BUILD)
+#error "K1 knock-out macros give wrong results: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
 #ifndef HHFM_K1_U5
 #define HHFM_K1_U5 5   // rows per lane in flight at F = 5
 #endif
@@ -99,7 +108,10 @@ __global__ __launch_bounds__(256) void fm_rows_fast(
       for (int f = 0; f < F; ++f) {
         id[u][f] = clamp_id(raw[u][f], M);
         bad |= id[u][f] != raw[u][f];
-        if (NTM == 2 && f < 2)
+        if (HHFM_K1_CTXKO && f >= 2) {
+#pragma unroll
+          for (int e = 0; e < C::kElems; ++e) c[u][f].v[e] = 0.f;
+        } else if (NTM == 2 && f < 2)
           c[u][f].template load<true>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);
         else
           c[u][f].template load<NT>(E + (int64_t)id[u][f] * ROW_BYTES + sub * 16);

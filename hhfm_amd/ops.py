@@ -162,6 +162,22 @@ def _workspace(dev: torch.device, nbytes: int) -> torch.Tensor:
     return buf
 
 
+_CWS = {}
+
+
+def _catalog_workspace(dev: torch.device, stream: int, nbytes: int) -> torch.Tensor:
+    """hhfm_catalog_topk's own workspace per (device, stream): zero-filled when
+    allocated, because its first HHFM_CATALOG_WS_ZERO bytes hold the
+    small-catalog kernel's arrival counters (include/hhfm.h, ABI v6: zero
+    before the first call, left zero by every call; no other op shares it)."""
+    key = (dev.index, stream)
+    buf = _CWS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+        _CWS[key] = buf
+    return buf
+
+
 def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
                  item_row_begin: int, item_count: int, global_item_base: int = 0,
                  w: Optional[torch.Tensor] = None, user_col: int = 0,
@@ -177,15 +193,15 @@ def catalog_topk(qidx: torch.Tensor, E: torch.Tensor, mode: int, K: int,
     B, ncols = qidx.shape
     M, k = E.shape
     nat = native()
-    ws_bytes = nat.catalog_topk_workspace(B, item_count, k, K)
-    ws = _workspace(dev, ws_bytes)
+    st = _stream(dev)
+    ws = _catalog_workspace(dev, st, nat.catalog_topk_workspace(B, item_count, k, K))
     top_s = torch.empty(B, K, dtype=torch.float32, device=dev)
     top_i = torch.empty(B, K, dtype=torch.int32, device=dev)
     nat.catalog_topk(qidx.data_ptr(), B, ncols, mode, user_col, ctx[0], ctx[1],
                      time[0], time[1], E.data_ptr(), M, k, _dtype_code(E),
                      0 if w is None else w.data_ptr(), item_row_begin, item_count,
                      global_item_base, K, top_s.data_ptr(), top_i.data_ptr(),
-                     ws.data_ptr(), ws.numel(), int(plan), _status_ptr(status), _stream(dev))
+                     ws.data_ptr(), ws.numel(), int(plan), _status_ptr(status), st)
     return top_s, top_i
 
 

@@ -30,7 +30,9 @@
 extern "C" {
 #endif
 
-#define HHFM_ABI_VERSION 5
+#define HHFM_ABI_VERSION 6
+/* leading workspace bytes of hhfm_catalog_topk(_ex) that must start zero */
+#define HHFM_CATALOG_WS_ZERO 16384
 
 enum hhfm_dtype { HHFM_F32 = 0, HHFM_BF16 = 1 };
 
@@ -165,7 +167,10 @@ int hhfm_hybrid_score_rows_ex(const int32_t* idx, int64_t B, int32_t ncols,
  *            k-ordered fp32 chain); plan HHFM_PLAN_EXACT_FP32 (the _ex form)
  *            selects the fp32-MFMA kernels (the k-ordered fmaf chain).
  * Workspace: query `hhfm_catalog_topk_workspace` with the same sizes (it
- * covers every plan).
+ * covers every plan).  Its first HHFM_CATALOG_WS_ZERO bytes must be zero
+ * before the first call (the small-catalog kernel's per-call arrival
+ * counters: every call leaves them zero again); a buffer used by other
+ * entry points in between must be re-zeroed there (ABI v6).
  * ---------------------------------------------------------------------- */
 int hhfm_catalog_topk_workspace(int64_t B, int32_t item_count, int32_t k,
                                 int32_t K, size_t* ws_bytes);

@@ -11,7 +11,7 @@ for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   mkdir -p ${AB_DIR:-ab}/$name
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-function \
-    $defs -c hhfm_amd/csrc/$src.hip -o build/var_$name.o
+    -DHHFM_DIAG_BUILD $defs -c hhfm_amd/csrc/$src.hip -o build/var_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ${AB_DIR:-ab}/$name/libhhfm.so $others build/var_$name.o
   cp hhfm_amd/lib/_hhfm*.so ${AB_DIR:-ab}/$name/
   rm build/var_$name.o

@@ -1,4 +1,4 @@
-"""Diagnostic (with a -DHHFM_FUSED_TIMING=1 build first on PYTHONPATH): the
+"""Diagnostic (with a -DHHFM_DIAG_BUILD -DHHFM_FUSED_TIMING=1 build first on PYTHONPATH): the
 fused small-catalog kernel's per-phase cycles per wave (s_memtime sums over
 every wave) at the C3 shape (HHFM k=64 bf16, Frappe 4,082 items, top-20) for
 300 and 3,000 queries."""
@@ -20,9 +20,9 @@ nu, ni, k = 957, 4082, 64
 M = nu + ni + 12
 E = (torch.randn(M, k, generator=g, device=dev) * 0.01).to(torch.bfloat16)
 buf = (ctypes.c_ulonglong * 8)()
-names = ["ids_queries", "b_operands", "scores", "threshold", "survivors", "sort_write"]
+names = ["query_phase", "scores", "threshold", "survivors", "range_sort"]
 res = {}
-for B in (300, 3000):
+for B in (300, 2048, 3000):
     cols = [torch.randint(0, nu, (B,), generator=g, device=dev),
             torch.randint(nu, nu + ni, (B,), generator=g, device=dev)]
     off = nu + ni
@@ -48,8 +48,9 @@ for B in (300, 3000):
     torch.cuda.synchronize()
     fn(buf)
     t = list(buf)
-    nw = max(t[6], 1)
+    nw = max(t[5], 1)
     res[f"B{B}"] = {"cycles_per_wave": {n: t[i] / nw for i, n in enumerate(names)},
-                    "waves_per_call": nw / 20,
+                    "waves_per_call": nw / 20, "merging_waves": t[6] / 20,
+                    "merge_cycles_per_merging_wave": t[7] / max(t[6], 1),
                     "call_us_median": sorted(a.elapsed_time(b) for a, b in ev)[10] * 1e3}
     print(json.dumps({f"B{B}": res[f"B{B}"]}), flush=True)

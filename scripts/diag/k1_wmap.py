@@ -42,5 +42,14 @@ def run(wt):   # the C ABI directly: the diagnostic w buffer is larger than M
                          0 if wt is None else wt.data_ptr(), 0.0, out.data_ptr(), 0, 0, st)
 
 
-res = {"with_w_ms": timeit(lambda: run(wbig)), "no_w_ms": timeit(lambda: run(None))}
+idx2 = idx[:, :2].contiguous()
+
+
+def run2(wt):   # user and item columns only (F = 2): the gather floor
+    nat.fm_score_rows_ex(idx2.data_ptr(), rows, 2, E.data_ptr(), M, 64, 0,
+                         0 if wt is None else wt.data_ptr(), 0.0, out.data_ptr(), 0, 0, st)
+
+
+res = {"with_w_ms": timeit(lambda: run(wbig)), "no_w_ms": timeit(lambda: run(None)),
+       "ui_w_ms": timeit(lambda: run2(wbig)), "ui_only_ms": timeit(lambda: run2(None))}
 print(json.dumps(res))

@@ -26,7 +26,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
     lib.hhfm_abi_version.restype = ctypes.c_int
-    assert lib.hhfm_abi_version() == 5
+    assert lib.hhfm_abi_version() == 6
 
 
 def test_pybind_module_binds_the_abi():
@@ -36,7 +36,7 @@ def test_pybind_module_binds_the_abi():
               "topk_merge", "topk_merge_host", "check_ids", "status_read",
               "probe_stream_read"]:
         assert hasattr(m, n)
-    assert m.abi_version() == 5
+    assert m.abi_version() == 6
 
 
 def test_argument_validation_without_device():
