@@ -88,12 +88,16 @@ def sharded_topk(A, K: int, n_item: int, local_scorer: LocalScorer, group=None):
         raise ValueError(f"K={K} exceeds the catalog size {n_item}")
     begin, end = shard_range(n_item, world, rank)
     count = end - begin
+    dev = comm_device(group)
     if count > 0:
         s, i = local_scorer(A, begin, count, min(K, count))
         s, i = _pad(s, i, K)
+        # the payload where the backend reads it: the GPU for RCCL, host
+        # memory for gloo (a device scorer's lists copied once, B·K·8 bytes)
+        if world > 1:
+            s, i = s.to(dev), i.to(dev)
     else:
         B = len(A)
-        dev = comm_device(group)
         s = torch.full((B, K), NEG_INF, dtype=torch.float32, device=dev)
         i = torch.full((B, K), NO_IDX, dtype=torch.int32, device=dev)
     if world == 1:
