@@ -52,19 +52,19 @@ namespace hhfm {
 #error "HHFM_FUSED_TIMING: diagnostic builds only (-DHHFM_DIAG_BUILD)"
 #endif
 #if HHFM_FUSED_TIMING
-// [0] query phase, [1] scores, [2] threshold, [3] survivors (+ overflow
-// rounds), [4] range sort and hand-off, [5] waves, [6] merging workgroups,
-// [7] merge
-__device__ unsigned long long g_fused_t[8];
-#define HHFM_TMARK(v) v = __builtin_amdgcn_s_memtime()
+// per workgroup, wave 0's s_memtime at kFusedMarks points (plain stores: no
+// atomics that would queue beside the hand-off); host side: differences
+constexpr int kFusedTimingWG = 16384, kFusedMarks = 24;
+__device__ unsigned long long g_fused_t[kFusedTimingWG][kFusedMarks];
+#define HHFM_MARK(i) tmk[i] = __builtin_amdgcn_s_memtime()
 #else
-#define HHFM_TMARK(v) (void)0
+#define HHFM_MARK(i) (void)0
 #endif
 
 constexpr int kFusedCap = 128;    // list entries held per query
 // arrival counters (one per 32 queries) at the workspace's start
 constexpr int kFusedMaxGroups = HHFM_CATALOG_WS_ZERO / 4;
-constexpr int kFusedMaxS = 16;    // item ranges (workgroups) per 32 queries
+constexpr int kFusedMaxS = 16;    // item ranges (workgroups) per 32 queries (merge: 4 unrolled)
 constexpr int kFusedTiles = 4;    // item tiles per wave: a range = 8 x 4 tiles = 1,024 items
 constexpr int kFusedMaxCtx = 8;   // context (and time) fields the fused kernel takes
 constexpr int kFusedWaves = 8;
@@ -167,7 +167,107 @@ HHFM_DEV float select16(const float (&v)[16], int r) {
   return __uint_as_float(bl(c[0], c[1], m3));
 }
 
-template <bool BF16, int KT, bool FM, bool SPLIT, int T>
+// ---- rolled networks -------------------------------------------------------
+// The kernel runs once per workgroup on a CU whose instruction cache the
+// dispatch has just emptied: every executed line is fetched from L2 (~290
+// fetches per workgroup, ~100 cycles per 64-B line measured), so an unrolled
+// network costs more in instruction fetch than in execution.  These loops
+// fetch one body; the partner exchange picks its DPP / swizzle / permlane
+// form behind a wave-uniform branch on d.
+HHFM_DEV void xor_lane2_rt(int32_t& a, int32_t& b, int d) {
+  if (d == 1) { a = xor_lane(a, 1); b = xor_lane(b, 1); }
+  else if (d == 2) { a = xor_lane(a, 2); b = xor_lane(b, 2); }
+  else if (d == 4) { a = xor_lane(a, 4); b = xor_lane(b, 4); }
+  else if (d == 8) { a = xor_lane(a, 8); b = xor_lane(b, 8); }
+  else if (d == 16) { a = xor_lane(a, 16); b = xor_lane(b, 16); }
+  else { a = xor_lane(a, 32); b = xor_lane(b, 32); }
+}
+HHFM_DEV uint64_t xor_lane64_rt(uint64_t v, int d) {
+  int32_t lo = (int32_t)(uint32_t)v, hi = (int32_t)(uint32_t)(v >> 32);
+  xor_lane2_rt(lo, hi, d);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// bitonic sort of keys, descending, in aligned groups of N lanes (rolled)
+template <int N>
+HHFM_DEV void sort_keys_rt(uint64_t& k) {
+  const int l = lane_id() & (N - 1);
+#pragma unroll 1
+  for (int size = 2; size <= N; size <<= 1) {
+    const bool desc = (l & size) == 0 || size == N;
+#pragma unroll 1
+    for (int d = size >> 1; d >= 1; d >>= 1) {
+      const uint64_t p = xor_lane64_rt(k, d);
+      const bool keep_max = ((l & d) == 0) == desc;
+      k = ((p > k) == keep_max) ? p : k;
+    }
+  }
+}
+// the best N of the union of two descending key lists (rolled merge_keys)
+template <int N>
+HHFM_DEV void merge_keys_rt(uint64_t& a, uint64_t b) {
+  const int l = lane_id();
+  const int src = (l & ~(N - 1)) | (N - 1 - (l & (N - 1)));
+  const uint32_t blo = (uint32_t)__shfl((int32_t)(uint32_t)b, src, kWave);
+  const uint32_t bhi = (uint32_t)__shfl((int32_t)(uint32_t)(b >> 32), src, kWave);
+  const uint64_t r = ((uint64_t)bhi << 32) | blo;
+  a = r > a ? r : a;
+  const int lg = l & (N - 1);
+#pragma unroll 1
+  for (int d = N >> 1; d >= 1; d >>= 1) {
+    const uint64_t p = xor_lane64_rt(a, d);
+    a = ((p > a) == ((lg & d) == 0)) ? p : a;
+  }
+}
+// two independent score sorts (descending, aligned groups of 32), rolled
+HHFM_DEV void sort_scores2_rt(float& s0, float& s1) {
+  const int l = lane_id() & 31;
+#pragma unroll 1
+  for (int size = 2; size <= 32; size <<= 1) {
+    const bool desc = (l & size) == 0 || size == 32;
+#pragma unroll 1
+    for (int d = size >> 1; d >= 1; d >>= 1) {
+      int32_t a = __float_as_int(s0), b = __float_as_int(s1);
+      xor_lane2_rt(a, b, d);
+      const bool keep_max = ((l & d) == 0) == desc;
+      const float p0 = __int_as_float(a), p1 = __int_as_float(b);
+      s0 = keep_max ? fmaxf(s0, p0) : fminf(s0, p0);
+      s1 = keep_max ? fmaxf(s1, p1) : fminf(s1, p1);
+    }
+  }
+}
+
+// network form (A/B knobs, default: unrolled DPP networks; rolled loops
+// measured slower — every stage's uniform branch chain and DPP hazard waits
+// cost more than the instruction fetch they save)
+#ifndef HHFM_FUSED_ROLLED
+#define HHFM_FUSED_ROLLED 0
+#endif
+template <int N>
+HHFM_DEV void sort_keys(uint64_t& k) {
+  if constexpr (HHFM_FUSED_ROLLED) sort_keys_rt<N>(k);
+  else sort_keys_desc<N>(k);
+}
+template <int N>
+HHFM_DEV void merge_keys_sel(uint64_t& a, uint64_t b) {
+  if constexpr (HHFM_FUSED_ROLLED) merge_keys_rt<N>(a, b);
+  else merge_keys<N>(a, b);
+}
+HHFM_DEV void sort_scores2(float& s0, float& s1) {
+  if constexpr (HHFM_FUSED_ROLLED) {
+    sort_scores2_rt(s0, s1);
+  } else {
+    float m[2] = {s0, s1};
+    sort_desc_scores_n<32, 2>(m);
+    s0 = m[0];
+    s1 = m[1];
+  }
+}
+
+// QL: the split query pieces in LDS (116 instead of 140 registers at C3: two
+// workgroups per CU, for grids past one workgroup per CU: 3,000 queries 33.0
+// -> 28.2 us) or in registers (one workgroup per CU: 300 queries 17.3 us
+// against 19.5 with QL)
+template <bool BF16, int KT, bool FM, bool SPLIT, int T, bool QL>
 __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     const int32_t* __restrict__ qidx, int64_t B, int ncols, int mode, int ucol, int c0, int c1,
     int t0, int t1, const char* __restrict__ E, int64_t M, int64_t item_row_begin, int32_t N,
@@ -186,6 +286,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   static_assert(T % PD == 0, "tiles per wave a multiple of the prefetch depth");
 
   __shared__ float hq[kQPerWave][k + 4];
+  __shared__ bf16x8 qps[SPLIT && QL ? 3 : 1][SPLIT && QL ? NU : 1][kWave];
+  __shared__ int32_t qid[kQPerWave][1 + 2 * kFusedMaxCtx];   // the queries' field ids
   __shared__ float cq_l[kQPerWave];
   __shared__ float pq[kQPerWave][64];   // FM: per query, catalog_queries' 64 lane values
   __shared__ float gmx[kQPerWave][33];  // per query the 32 offered group values
@@ -207,26 +309,24 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   int rnd = 0;   // survivor rounds so far (selects the overflow flag word)
 
 #if HHFM_FUSED_TIMING
-  uint64_t tm0 = 0, tm1 = 0, tacc[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tmk[kFusedMarks] = {};
 #endif
-  HHFM_TMARK(tm0);
+  HHFM_MARK(0);
   // the query rows' raw ids first (8 threads per query; only the first 256
-  // threads form queries): their loads are the oldest, so waiting for them
-  // leaves the tile loads below in flight (vmcnt counts in order)
-  const int pq_q = threadIdx.x >> 3;
+  // threads form queries): thread tp of a query loads its fields tp, tp + 8,
+  // tp + 16 (field 0 the user, then the context and the time columns).  These
+  // are the oldest loads, so waiting for them leaves the tile loads below in
+  // flight (vmcnt counts in order)
+  const int pq_q = threadIdx.x >> 3, pq_t = threadIdx.x & 7;
   const int64_t pq_b = q0 + pq_q;
   const bool pq_on = threadIdx.x < 8 * kQPerWave && pq_b < B;
-  int32_t idu = 0, idc[kFusedMaxCtx], idt[kFusedMaxCtx];
+  const int nc = c1 - c0, nt = t1 - t0, nf = 1 + nc + nt;
+  int32_t rid[3];
 #pragma unroll
-  for (int f = 0; f < kFusedMaxCtx; ++f) idc[f] = idt[f] = 0;
-  if (pq_on) {
-    const int32_t* p = qidx + pq_b * (int64_t)ncols;
-    idu = p[ucol];
-#pragma unroll
-    for (int f = 0; f < kFusedMaxCtx; ++f) {
-      if (f < c1 - c0) idc[f] = p[c0 + f];
-      if (f < t1 - t0) idt[f] = p[t0 + f];
-    }
+  for (int x = 0; x < 3; ++x) {
+    const int f = pq_t + 8 * x;
+    const int col = f == 0 ? ucol : (f <= nc ? c0 + f - 1 : t0 + f - 1 - nc);
+    rid[x] = (pq_on && f < nf) ? qidx[pq_b * ncols + col] : 0;
   }
   asm volatile("" ::: "memory");   // keep the tile loads behind them
   // the wave's tile tt -> catalog tile (clamped: every load is issued, so
@@ -247,11 +347,19 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     for (int t = 0; t < KT; ++t) a[t] = *reinterpret_cast<const uint4*>(row + 32 * t);
     if constexpr (FM) wv_ = w ? w[item_row_begin + item_of(tile)] : 0.f;
   };
+  // the first PD tiles: at once in the waves that form no query (4..7);
+  // behind the query row loads in the others (0..3), whose wait for those
+  // rows would otherwise drain 8 KB of tile loads per wave first (vmcnt
+  // counts in order: 5.3K -> ~2K cycles measured for the row phase)
+  auto issue_tiles = [&]() {
 #pragma unroll
-  for (int d = 0; d < PD; ++d) {
-    wr[d] = 0.f;
-    load_tile(tile_of(d), ar[d], wr[d]);
-  }
+    for (int d = 0; d < PD; ++d) {
+      wr[d] = 0.f;
+      load_tile(tile_of(d), ar[d], wr[d]);
+    }
+  };
+  const bool qwave = wv * kWave < 8 * kQPerWave;   // this wave forms queries
+  if (!qwave) issue_tiles();
 
   // ---- 0. query vectors (catalog_queries' arithmetic, bit for bit) ----
   // 8 threads per query; thread tp loads 16-B chunks tp, tp + 8, ... of each
@@ -263,15 +371,15 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   {
     constexpr int CPR = k / EPC;              // 16-B chunks per row
     constexpr int CPT = (CPR + 7) / 8;        // chunks per thread
-    const int qq = threadIdx.x >> 3, tp = threadIdx.x & 7;
+    const int qq = pq_q, tp = pq_t;
     const int64_t b = q0 + qq;
     if (threadIdx.x < 8 * kQPerWave) {
-      idu = clamp_id(idu, M);
+      // the query's (clamped) field ids through LDS: the 8 threads of a query
+      // are lanes of one wave, and a wave's LDS accesses complete in order
 #pragma unroll
-      for (int f = 0; f < kFusedMaxCtx; ++f) {
-        idc[f] = clamp_id(idc[f], M);
-        idt[f] = clamp_id(idt[f], M);
-      }
+      for (int x = 0; x < 3; ++x)
+        if (tp + 8 * x < nf) qid[qq][tp + 8 * x] = clamp_id(rid[x], M);
+      HHFM_MARK(1);   // the ids arrived
       // lane L = e mod 64 accumulates e, then e + 64: chunk slot cc % LPT
       constexpr int LPT = 64 / (8 * EPC) > 0 ? 64 / (8 * EPC) : 1;
       float part[LPT][EPC];
@@ -292,52 +400,44 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           x[2] = __uint_as_float(u.z); x[3] = __uint_as_float(u.w);
         }
       };
-      const int nc = c1 - c0, nt = t1 - t0;
 #pragma unroll
       for (int cc = 0; cc < CPT; ++cc) {
         const int ch = tp + 8 * cc;
         if (ch < CPR) {
-          auto ld = [&](int32_t id) {
-            return *reinterpret_cast<const uint4*>(E + (int64_t)id * ROWB + 16 * ch);
+          auto ld = [&](int f) {
+            return *reinterpret_cast<const uint4*>(E + (int64_t)qid[qq][f] * ROWB + 16 * ch);
           };
-          // every field row of a chunk loaded before any is summed (one memory
-          // latency, not one per field)
-          const uint4 ru = ld(idu);
-          uint4 rc[kFusedMaxCtx], rt[kFusedMaxCtx];
-#pragma unroll
-          for (int f = 0; f < kFusedMaxCtx; ++f) {
-            rc[f] = make_uint4(0, 0, 0, 0);
-            rt[f] = make_uint4(0, 0, 0, 0);
-            if (f < nc) rc[f] = ld(idc[f]);
-            if (f < nt) rt[f] = ld(idt[f]);
-          }
+          // the user row, then the context and the time fields in field order,
+          // four rows in flight per step (rolled: one body fetched)
           float uu[EPC], cx[EPC], tm[EPC], r[EPC];
+          const uint4 ru = ld(0);
+#pragma unroll
+          for (int v = 0; v < EPC; ++v) cx[v] = tm[v] = 0.f;
+#pragma unroll 1
+          for (int f0 = 1; f0 < nf; f0 += 4) {
+            uint4 rr[4];
+#pragma unroll
+            for (int x = 0; x < 4; ++x) rr[x] = ld(f0 + x < nf ? f0 + x : 0);
+#pragma unroll
+            for (int x = 0; x < 4; ++x) {
+              const int f = f0 + x;   // wave-uniform
+              if (f >= nf) break;
+              cvt(rr[x], r);
+              if (f <= nc) {
+#pragma unroll
+                for (int v = 0; v < EPC; ++v) cx[v] += r[v];
+              } else {
+#pragma unroll
+                for (int v = 0; v < EPC; ++v) tm[v] += r[v];
+              }
+            }
+          }
           cvt(ru, uu);
-#pragma unroll
-          for (int v = 0; v < EPC; ++v) {
-            cx[v] = 0.f;
-            tm[v] = 0.f;
-          }
-          // ctx fields, then time fields, in field order
-#pragma unroll
-          for (int f = 0; f < kFusedMaxCtx; ++f) {
-            if (f >= nc) break;
-            cvt(rc[f], r);
-#pragma unroll
-            for (int v = 0; v < EPC; ++v) cx[v] += r[v];
-          }
-#pragma unroll
-          for (int f = 0; f < kFusedMaxCtx; ++f) {
-            if (f >= nt) break;
-            cvt(rt[f], r);
-#pragma unroll
-            for (int v = 0; v < EPC; ++v) tm[v] += r[v];
-          }
 #pragma unroll
           for (int v = 0; v < EPC; ++v) {
             float hv = 0.f;
             if (b < B) {
-              if (mode == HHFM_MODE_FM) {
+              if constexpr (FM) {
                 hv = uu[v] + cx[v];                     // FM.py:177
                 part[cc % LPT][v] += hv * cx[v];        // FM.py:178-183
               } else {
@@ -350,7 +450,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           }
         }
       }
-      if (mode == HHFM_MODE_FM) {
+      if constexpr (FM) {
 #pragma unroll
         for (int c = 0; c < LPT; ++c) {
           const int ch = tp + 8 * c;
@@ -360,6 +460,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         }
       }
     }
+    HHFM_MARK(2);   // rows loaded, hq written
+    if (qwave) issue_tiles();
     if (threadIdx.x < kQPerWave) {
       cnt[threadIdx.x] = 0;
       // the lowest finite score: items past N (held as -inf) never pass
@@ -367,7 +469,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     }
     if (threadIdx.x < 2) ovf[threadIdx.x] = 0;
     lds_barrier();
-    if (mode == HHFM_MODE_FM) {
+    HHFM_MARK(3);
+    if constexpr (FM) {
       for (int q2 = wv; q2 < kQPerWave; q2 += NW) {
         float x = l < k ? pq[q2][l] : 0.f;
         x = group_sum<kWave>(x);
@@ -377,33 +480,49 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     }
   }
 
-  // B operand (catalog_main): this lane's query j, k slices {EPC(2t+h) ..}
+  // B operand (catalog_main): this lane's query j, k slices {EPC(2t+h) ..}.
+  // Split-bf16: the three pieces are the same for every wave, so wave u
+  // splits k slice u once for the workgroup into LDS and every wave reads
+  // them per tile (48 fewer registers per lane: two workgroups fit a CU)
   float bq[KT][EPC];
+  bf16x8 qp[3][QL ? 1 : NU];
+  if constexpr (!SPLIT) {
 #pragma unroll
-  for (int t = 0; t < KT; ++t)
+    for (int t = 0; t < KT; ++t)
 #pragma unroll
-    for (int e = 0; e < EPC; ++e) bq[t][e] = hq[j][(2 * t + h) * EPC + e];
-  bf16x8 qp[3][NU];
-  if constexpr (SPLIT) {
+      for (int e = 0; e < EPC; ++e) bq[t][e] = hq[j][(2 * t + h) * EPC + e];
+  } else if constexpr (!QL) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       float x[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        if constexpr (BF16) x[e] = bq[u][e];
-        else x[e] = bq[2 * u + (e >> 2)][e & 3];
+        const int t = BF16 ? u : 2 * u + (e >> 2), ee = BF16 ? e : (e & 3);
+        x[e] = hq[j][(2 * t + h) * EPC + ee];
       }
       split3x8(x, qp[0][u], qp[1][u], qp[2][u]);
     }
+  } else {
+#pragma unroll 1
+    for (int u = wv; u < NU; u += NW) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int t = BF16 ? u : 2 * u + (e >> 2), ee = BF16 ? e : (e & 3);
+        x[e] = hq[j][(2 * t + h) * EPC + ee];
+      }
+      bf16x8 a0, a1, a2;
+      split3x8(x, a0, a1, a2);
+      qps[0][u][l] = a0;
+      qps[1][u][l] = a1;
+      qps[2][u][l] = a2;
+    }
+    lds_barrier();
   }
   const float cq = FM ? cq_l[j] : 0.f;
-#if HHFM_FUSED_TIMING
-  HHFM_TMARK(tm1);
-  tacc[0] += tm1 - tm0;
-#endif
+  HHFM_MARK(4);   // B operands ready
 
   {
-    HHFM_TMARK(tm0);
     // ---- 1. scores of this wave's T tiles, kept in registers ----
     float sc[T][16];
 #pragma unroll
@@ -415,14 +534,22 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       const char* nrow = E + (item_row_begin + item_of(nxt)) * ROWB + 16 * h;
       f32x16 acc = {0};
       const float wcur = wr[tt % PD];
+      // this tile's view of the piece array (laundered: the reads stay per
+      // tile instead of being hoisted into 48 live registers)
+      const bf16x8* qv = &qps[0][0][l];
+      if constexpr (QL) asm volatile("" : "+v"(qv));
+      auto QP = [&](int pc, int u) {
+        if constexpr (QL) return qv[(pc * NU + u) * kWave];
+        else return qp[pc][u];
+      };
       if constexpr (SPLIT && BF16) {
 #pragma unroll
         for (int t = 0; t < KT; ++t) {
           const bf16x8 ai = __builtin_bit_cast(bf16x8, ar_[t]);
           ar_[t] = *reinterpret_cast<const uint4*>(nrow + 32 * t);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[2][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[1][t], acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, qp[0][t], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(2, t), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(1, t), acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ai, QP(0, t), acc, 0, 0, 0);
         }
       } else if constexpr (SPLIT) {
 #pragma unroll
@@ -435,7 +562,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           ar_[2 * u + 1] = *reinterpret_cast<const uint4*>(nrow + 32 * (2 * u + 1));
           bf16x8 i0, i1, i2;
           split3x8(x, i0, i1, i2);
-          const bf16x8 p0 = qp[0][u], p1 = qp[1][u], p2 = qp[2][u];
+          const bf16x8 p0 = QP(0, u), p1 = QP(1, u), p2 = QP(2, u);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i2, p0, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i1, p1, acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(i0, p2, acc, 0, 0, 0);
@@ -483,11 +610,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       // one tile in flight: keeps the compiler from hoisting later tiles' loads
       asm volatile("" ::: "memory");
     }
-#if HHFM_FUSED_TIMING
-    HHFM_TMARK(tm1);
-    tacc[1] += tm1 - tm0;
-    tm0 = tm1;
-#endif
+    HHFM_MARK(5);   // scores in registers
 
     // ---- 2. threshold: K-th largest of the 32 offered tile maxima ----
     {
@@ -509,13 +632,16 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
 #pragma unroll
       for (int r = 0; r < R; ++r) gmx[j][(wv * 2 + h) * R + r] = mr[r];
     }
+    HHFM_MARK(6);
     lds_barrier();
+    HHFM_MARK(7);
     {   // wave wv: queries QW wv + 2u + h, one per 32-lane half
       constexpr int QW = kQPerWave / NW, U = QW / 2;
       float m[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) m[u] = gmx[wv * QW + 2 * u + h][j];
-      sort_desc_scores_n<32, U>(m);
+      static_assert(U == 2, "two queries per lane half");
+      sort_scores2(m[0], m[1]);
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const float t = shfl_f(m[u], (h << 5) + K - 1);
@@ -526,12 +652,9 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       }
     }
     if (threadIdx.x < kQPerWave) cprev[threadIdx.x] = cnt[threadIdx.x];
+    HHFM_MARK(8);
     lds_barrier();
-#if HHFM_FUSED_TIMING
-    HHFM_TMARK(tm1);
-    tacc[2] += tm1 - tm0;
-    tm0 = tm1;
-#endif
+    HHFM_MARK(9);   // threshold set
 
     // ---- 3. survivors to the per-query lists (re-filtered on overflow) ----
     const int qbase = j * kQS;
@@ -554,12 +677,17 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       // a score threshold (low word 0 on every lane) is `score >= t` (items
       // past N hold -inf); a raised pair threshold takes the key test
       if (__ballot(mine && tlo != 0) == 0) {
+        // per row its bit (v_cmp + v_cndmask with the bit as a literal), then
+        // a 3-input OR tree: depth 4 instead of a 16-long dependent chain
 #pragma unroll
         for (int tt = 0; tt < T; ++tt) {
-          uint32_t m = 0;
+          uint32_t bb[16];
 #pragma unroll
-          for (int r = 15; r >= 0; --r) m = m + m + (sc[tt][r] >= ts ? 1u : 0u);
-          pm[tt] = m;
+          for (int r = 0; r < 16; ++r) bb[r] = sc[tt][r] >= ts ? (1u << r) : 0u;
+          const uint32_t o0 = bb[0] | bb[1] | bb[2], o1 = bb[3] | bb[4] | bb[5];
+          const uint32_t o2 = bb[6] | bb[7] | bb[8], o3 = bb[9] | bb[10] | bb[11];
+          const uint32_t o4 = bb[12] | bb[13] | bb[14];
+          pm[tt] = (o0 | o1 | o2) | (o3 | o4 | bb[15]);
         }
       } else {
         // key >= (ukey(ts), ~ti)  <=>  x > ts, or x == ts and index <= ti
@@ -580,28 +708,43 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       int n = 0;
 #pragma unroll
       for (int tt = 0; tt < T; ++tt) n += __popc(pm[tt]);
+      if (first) HHFM_MARK(10);
       int pos = atomicAdd(&cnt[j], n);
+      if (first) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        HHFM_MARK(11);
+      }
       asm volatile("" : "+v"(ib));   // recompute the indices below (no 16 T live values)
-      // one survivor per lane per step (lowest row first); a lane without one
+      // per step one survivor of every tile per lane (lowest row first; the
+      // four extractions independent of each other); a lane without one
       // writes the query's spare slot (no exec-mask branches)
+      uint32_t mt[T];
 #pragma unroll
-      for (int tt = 0; tt < T; ++tt) {
-        uint32_t m = pm[tt];
+      for (int tt = 0; tt < T; ++tt) mt[tt] = pm[tt];
+      uint32_t any = 0;
+#pragma unroll
+      for (int tt = 0; tt < T; ++tt) any |= mt[tt];
 #pragma unroll 1
-        while (__ballot(m != 0) != 0) {
+      while (__ballot(any != 0) != 0) {
+        any = 0;
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+          const uint32_t m = mt[tt];
           const int r = __builtin_ctz(m | 0x10000u) & 15;
           const float x = select16(sc[tt], r);
           const int32_t it = ib + tt * kTile + (r & 3) + 8 * (r >> 2);
           const int slot = m ? (pos < kFusedCap ? pos : kFusedCap) : kFusedCap;
           cbuf[qbase + slot] = ekey(x, it);
           pos += m ? 1 : 0;
-          m &= m - 1;
+          mt[tt] = m & (m - 1);
+          any |= mt[tt];
         }
       }
       // a lane whose last slot lies past the cap flags the overflow in this
       // round's flag word (two words alternate, so the reset of the next
       // round's word never races with this round's writers)
       if (pos > kFusedCap) ovf[rnd & 1] = 1;
+      if (first) HHFM_MARK(12);
       lds_barrier();
       const bool over = ovf[rnd & 1] != 0;
       if (threadIdx.x == 0) ovf[(rnd + 1) & 1] = 0;   // last read before this barrier
@@ -620,9 +763,9 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         if (!of) continue;
         const uint64_t e0 = cbuf[qq * kQS + l], e1 = cbuf[qq * kQS + l + 64];
         uint64_t k0 = e0, k1 = e1;
-        sort_keys_desc<64>(k0);
-        sort_keys_desc<64>(k1);
-        merge_keys<64>(k0, k1);   // the best 64 of the 128, sorted
+        sort_keys<64>(k0);
+        sort_keys<64>(k1);
+        merge_keys_sel<64>(k0, k1);   // the best 64 of the 128, sorted
         const uint32_t nlo = __builtin_amdgcn_readlane((int32_t)(uint32_t)k0, K - 1);
         const uint32_t nhi = __builtin_amdgcn_readlane((int32_t)(uint32_t)(k0 >> 32), K - 1);
         const uint64_t nk = ((uint64_t)nhi << 32) | nlo;
@@ -647,10 +790,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       }
       lds_barrier();
     }
-#if HHFM_FUSED_TIMING
-    HHFM_TMARK(tm1);
-    tacc[3] += tm1 - tm0;
-#endif
+    HHFM_MARK(13);   // survivors listed
   }
 
   // ---- 4. per query: the range's entries at or above the final threshold,
@@ -660,7 +800,6 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
   // wave's LDS scratch and one 32-lane key network sorts them (typically
   // ~K·1.2 pass).  A query with more than 32 passing takes the 64-lane
   // network (+ merges past 64), one query at a time.
-  HHFM_TMARK(tm0);
   typedef __attribute__((address_space(1))) uint64_t gu64;
   typedef __attribute__((address_space(1))) uint32_t gu32;
   // rank r of query qq: the output (S = 1) or the range's list, stored
@@ -697,9 +836,11 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         if (ok && nv + pre < 32) fscr[wv][(h << 5) + nv + pre] = e;
         nv += __popc(hm);
       }
+      if (u == 0) HHFM_MARK(14);
       if (__ballot(nv > 32) == 0) {
         uint64_t key = j < nv ? fscr[wv][(h << 5) + j] : 0ull;
-        sort_keys_desc<32>(key);
+        sort_keys<32>(key);
+        if (u == 0) HHFM_MARK(15);
         emit(qq, j, key);
       } else {   // rare: one query at a time over the whole wave
 #pragma unroll 1
@@ -712,9 +853,9 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
           for (int c = 0; c < n2; c += kWave) {
             const uint64_t e = cbuf[q2 * kQS + (c + l < n2 ? c + l : kFusedCap)];
             uint64_t key = (c + l < n2 && e >= t2) ? e : 0ull;
-            sort_keys_desc<64>(key);
+            sort_keys<64>(key);
             if (c == 0) top = key;
-            else merge_keys<32>(top, key);
+            else merge_keys_sel<32>(top, key);
             if (l >= 32) top = 0;
           }
           if (l < 32) emit(q2, l, top);
@@ -722,11 +863,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       }
     }
   }
-#if HHFM_FUSED_TIMING
-  HHFM_TMARK(tm1);
-  tacc[4] += tm1 - tm0;
-  tm0 = tm1;
-#endif
+  HHFM_MARK(16);   // range lists emitted
 
   // ---- 5. S > 1: hand-off, the last arriving workgroup merges ----
   bool merged = false;
@@ -734,46 +871,67 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     // every storing wave drains its sc1 stores, then the barrier, then ONE
     // lane's agent-scope add for the whole workgroup
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    HHFM_MARK(17);
     lds_barrier();
+    HHFM_MARK(18);
     if (threadIdx.x == 0) {
       const uint32_t old = __hip_atomic_fetch_add((gu32*)(arrive + g), 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
       last_sh = old == (uint32_t)(S - 1);
     }
+    HHFM_MARK(19);
     lds_barrier();
+    HHFM_MARK(20);
     merged = last_sh != 0;   // uniform
     if (merged) {
       // no instruction: keeps the sc1 loads below the barrier
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       constexpr int QW = kQPerWave / NW;
-      constexpr int kMaxS = kFusedMaxS;
-#pragma unroll 1
-      for (int u = 0; u < QW; ++u) {
-        const int qq = wv * QW + u;
-        // lane (h, j) holds rank j of the lists h, h + 2, ...: all loads in
-        // flight before the merges
-        uint64_t v[kMaxS / 2];
-#pragma unroll
-        for (int x = 0; x < kMaxS / 2; ++x) {
-          const int sl = 2 * x + h;
-          v[x] = 0;
-          if (2 * x < S) {   // wave-uniform
-            const gu64* src =
-                (const gu64*)(part + ((((int64_t)g * S + (sl < S ? sl : 0)) * kQPerWave + qq) << 5) + j);
-            const uint64_t t = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[x] = sl < S ? t : 0ull;
-          }
-        }
-        uint64_t a = v[0];
-#pragma unroll
-        for (int x = 1; x < kMaxS / 2; ++x)
-          if (2 * x < S) merge_keys<32>(a, v[x]);
+      // lane (h, j) holds rank j of the lists h, h + 2, ... of the wave's QW
+      // queries; up to 4 lists per query every load is issued before any
+      // merge (one memory latency; merged from registers — a rolled merge
+      // staged through LDS measured 60 % slower), more take a rolled loop
+      auto src = [&](int u, int sl) {
+        return (const gu64*)(part + ((((int64_t)g * S + (sl < S ? sl : 0)) * kQPerWave +
+                                      wv * QW + u) << 5) + j);
+      };
+      auto finish = [&](int u, uint64_t a) {
         merge_keys<32>(a, xor_lane64(a, 32));   // the odd lists' half into the even's
-        const int64_t b = q0 + qq;
+        const int64_t b = q0 + wv * QW + u;
         if (b < B && l < K) {
           out_s[b * K + l] = ukey_inv((uint32_t)(a >> 32));
           const int32_t it = ~(int32_t)(uint32_t)a;
           out_i[b * K + l] = it == kNoIdx ? kNoIdx : it + gbase;
+        }
+      };
+      if (S <= 4) {
+        uint64_t v[QW][2];
+#pragma unroll
+        for (int u = 0; u < QW; ++u)
+#pragma unroll
+          for (int x = 0; x < 2; ++x) {
+            const int sl = 2 * x + h;
+            v[u][x] = __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[u][x] = sl < S ? v[u][x] : 0ull;
+          }
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          uint64_t a = v[u][0];
+          if (S > 2) merge_keys<32>(a, v[u][1]);
+          finish(u, a);
+        }
+      } else {
+#pragma unroll 1
+        for (int u = 0; u < QW; ++u) {
+          uint64_t a = 0;
+#pragma unroll 1
+          for (int x = 0; 2 * x < S; ++x) {
+            const int sl = 2 * x + h;
+            const uint64_t t =
+                __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            merge_keys_sel<32>(a, sl < S ? t : 0ull);
+          }
+          finish(u, a);
         }
       }
       // re-arm the counter for the next call (stream order publishes it)
@@ -781,17 +939,13 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
         __hip_atomic_store((gu32*)(arrive + g), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  HHFM_MARK(21);
 #if HHFM_FUSED_TIMING
-  HHFM_TMARK(tm1);
-  tacc[5] += tm1 - tm0;
-  if (l == 0) {
+  if (threadIdx.x == 0 && blockIdx.x < kFusedTimingWG) {
+    tmk[22] = merged ? 1ull : 0ull;
+    tmk[23] = 1ull;
 #pragma unroll
-    for (int p = 0; p < 5; ++p) atomicAdd(&g_fused_t[p], tacc[p]);
-    atomicAdd(&g_fused_t[5], 1ull);
-    if (merged) {
-      atomicAdd(&g_fused_t[6], 1ull);
-      atomicAdd(&g_fused_t[7], tacc[5]);
-    }
+    for (int p = 0; p < kFusedMarks; ++p) g_fused_t[blockIdx.x][p] = tmk[p];
   }
 #endif
   (void)merged;

@@ -62,6 +62,9 @@ constexpr int64_t kSeedBudget[2] = {kSeedMax[0] * 1024, kSeedMax[1] * 1024};
 // catalog_ring bf16 tile slots: R-1 tiles of DMA lead, or (pairs) R-2
 #define HHFM_RING_SLOTS (HHFM_RING_PAIR ? 6 : 4)
 #endif
+#ifndef HHFM_FUSED_T2
+#define HHFM_FUSED_T2 0   // fused kernel: 2-tile ranges at few queries (A/B knob)
+#endif
 #ifndef HHFM_MAIN_PF
 #define HHFM_MAIN_PF 1   // item tiles in flight per wave (1 or 2)
 #endif
@@ -990,7 +993,7 @@ struct Plan {
   int seed_n;            // streaming path: items of the threshold seed (0 = none)
   int rnqb[2], rS[2], rtps[2];   // catalog_ring with 4 / 8 waves: query groups, splits, tiles
   int sS[2], stps[2];            // the same over the seed's items (its GMAX pass)
-  int fS;                // fused small-catalog kernel: workgroups (item ranges) per 32 queries
+  int fS, fT;            // fused small-catalog kernel: workgroups (item ranges) per 32 queries, tiles per wave
   size_t off_H, off_cst, off_thr, off_ps, off_pi, off_sc, off_seed_sc, off_seed_s,
       off_seed_i, total;
 };
@@ -1067,7 +1070,17 @@ static Plan make_plan(int64_t B, int32_t N, int32_t k, int32_t K, int32_t plan, 
   p.off_sc = off;
   // the fused kernel's range lists [groups][S][32 queries][32] keys share the
   // score matrix's region (never both in one call)
-  p.fS = (ntiles + kFusedWaves * kFusedTiles - 1) / (kFusedWaves * kFusedTiles);
+  // ranges of 8 x 2 tiles (512 items) while the grid stays within one
+  // workgroup per CU, else 8 x 4 tiles: more CUs per query group at few
+  // queries (the per-workgroup latency chain is the cost there)
+  {
+    const int nqb = (int)((B + kQPerWave - 1) / kQPerWave);
+    const int s2 = (ntiles + kFusedWaves * 2 - 1) / (kFusedWaves * 2);
+    // (2-tile ranges measured slower at 300 queries: 22.5 vs 17.4 us — the
+    // merge of 8 lists per query outweighs the shorter ranges; kept off)
+    p.fT = HHFM_FUSED_T2 && (int64_t)nqb * s2 <= 256 && s2 <= kFusedMaxS ? 2 : kFusedTiles;
+    p.fS = (ntiles + kFusedWaves * p.fT - 1) / (kFusedWaves * p.fT);
+  }
   if (p.dense) {
     const size_t sc_bytes = (size_t)B * p.ldsc * sizeof(float);
     const size_t fl_bytes = p.fS > 1 ? (size_t)((B + kQPerWave - 1) / kQPerWave) * p.fS *
@@ -1230,32 +1243,52 @@ static void launch_store(int64_t B, int nqb, int32_t N, const float* H, const fl
 // the fused small-catalog kernel (catalog_fused.h): S 8-wave workgroups per
 // 32 queries, each over one range of 8 x kFusedTiles item tiles; the last to
 // finish merges the S range lists
-template <bool BF16, int KT, bool FM>
-static void launch_fused(int64_t B, int S, const int32_t* qidx, int ncols, int mode, int ucol,
+template <bool BF16, int KT, bool FM, int T>
+static void launch_fused_t(int64_t B, int S, const int32_t* qidx, int ncols, int mode, int ucol,
                          int c0, int c1, int t0, int t1, const char* E, int64_t M, int64_t irb,
                          int32_t N, const float* w, int K, float* os, int32_t* oi, int32_t gbase,
                          uint32_t* arrive, uint64_t* part, int32_t plan, hipStream_t st) {
   constexpr bool kCanSplit = BF16 || KT >= 2;
-  constexpr int T = kFusedTiles;
   const int nqb = (int)((B + kQPerWave - 1) / kQPerWave);
-  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32))
-    hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, kCanSplit, T>), dim3(nqb * S),
-                       dim3(kFusedWaves * 64), 0, st, qidx, B, ncols, mode, ucol, c0, c1, t0, t1,
-                       E, M, irb, N, w, K, os, oi, gbase, S, arrive, part);
+  // past one workgroup per CU the split query pieces move to LDS (two
+  // workgroups per CU); below it they stay in registers
+  const bool ql = (int64_t)nqb * S > 256;
+#define HHFM_FL(SP, QL_)                                                                       \
+  hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, SP, T, QL_>), dim3(nqb * S),                 \
+                     dim3(kFusedWaves * 64), 0, st, qidx, B, ncols, mode, ucol, c0, c1, t0, t1, \
+                     E, M, irb, N, w, K, os, oi, gbase, S, arrive, part)
+  if (kCanSplit && !(plan & HHFM_PLAN_EXACT_FP32)) {
+    if (ql) HHFM_FL(kCanSplit, true);
+    else HHFM_FL(kCanSplit, false);
+  } else {
+    HHFM_FL(false, false);
+  }
+#undef HHFM_FL
+}
+
+template <bool BF16, int KT, bool FM>
+static void launch_fused(int64_t B, int S, int T, const int32_t* qidx, int ncols, int mode,
+                         int ucol, int c0, int c1, int t0, int t1, const char* E, int64_t M,
+                         int64_t irb, int32_t N, const float* w, int K, float* os, int32_t* oi,
+                         int32_t gbase, uint32_t* arrive, uint64_t* part, int32_t plan,
+                         hipStream_t st) {
+  if (T == 2)
+    launch_fused_t<BF16, KT, FM, 2>(B, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N,
+                                    w, K, os, oi, gbase, arrive, part, plan, st);
   else
-    hipLaunchKernelGGL((catalog_fused<BF16, KT, FM, false, T>), dim3(nqb * S),
-                       dim3(kFusedWaves * 64), 0, st, qidx, B, ncols, mode, ucol, c0, c1, t0, t1,
-                       E, M, irb, N, w, K, os, oi, gbase, S, arrive, part);
+    launch_fused_t<BF16, KT, FM, kFusedTiles>(B, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E,
+                                              M, irb, N, w, K, os, oi, gbase, arrive, part, plan,
+                                              st);
 }
 
 template <bool BF16, bool FM>
-static bool dispatch_fused(int KT, int64_t B, int S, const int32_t* qidx, int ncols, int mode,
+static bool dispatch_fused(int KT, int64_t B, int S, int T, const int32_t* qidx, int ncols, int mode,
                            int ucol, int c0, int c1, int t0, int t1, const char* E, int64_t M,
                            int64_t irb, int32_t N, const float* w, int K, float* os, int32_t* oi,
                            int32_t gbase, uint32_t* arrive, uint64_t* part, int32_t plan,
                            hipStream_t st) {
 #define HHFM_FUSED(KT_) \
-  launch_fused<BF16, KT_, FM>(B, S, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, \
+  launch_fused<BF16, KT_, FM>(B, S, T, qidx, ncols, mode, ucol, c0, c1, t0, t1, E, M, irb, N, w, K, \
                               os, oi, gbase, arrive, part, plan, st)
   switch (KT) {
     case 1: HHFM_FUSED(1); break;
@@ -1419,7 +1452,7 @@ extern "C" int hhfm_catalog_topk_ex(
     const float* wv = (fmm && w) ? w : nullptr;
     uint32_t* arrive = reinterpret_cast<uint32_t*>(ws);
     uint64_t* part = reinterpret_cast<uint64_t*>(ws + p.off_sc);
-#define HHFM_FARGS KT, B, p.fS, qidx, ncols, mode, user_col, ctx_begin, ctx_end, time_begin, \
+#define HHFM_FARGS KT, B, p.fS, p.fT, qidx, ncols, mode, user_col, ctx_begin, ctx_end, time_begin, \
     time_end, Eb, features_M, (int64_t)item_row_begin, item_count, wv, K, top_score, top_idx, \
     global_item_base, arrive, part, plan, st
     const bool ok = bf16 ? (fmm ? dispatch_fused<true, true>(HHFM_FARGS)
@@ -1551,11 +1584,15 @@ extern "C" int hhfm_catalog_topk_ex(
 }
 
 #if HHFM_FUSED_TIMING
-// diagnostic builds only: read and clear the fused kernel's phase sums
+// diagnostic builds only: read and clear the fused kernel's per-workgroup
+// phase stamps (out: kFusedTimingWG x kFusedMarks)
 extern "C" int hhfm_debug_fused_timing(unsigned long long* out) {
-  hipDeviceSynchronize();
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fused_t), sizeof(g_fused_t)) != hipSuccess) return -1;
-  static const unsigned long long zero[8] = {0};
+  return 0;
+}
+extern "C" int hhfm_debug_fused_timing_clear(void) {
+  static unsigned long long zero[kFusedTimingWG][kFusedMarks];
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fused_t), zero, sizeof(zero));
 }
 #endif
