@@ -509,7 +509,7 @@ def _c4_parity(E, check_rows, Aq, s, i, world, row0, ni, k, table_dtype, dev):
     return par
 
 
-def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
+def c5_leg(dev, world, rank, rows, reps=5, warm=3, mlp=torch.bfloat16, check=True):
     """configs[4] / C5: DeepFM F=5, k=256, MLP 3x400 (DFM.py:104-137),
     Frappe vocabulary, `rows` rows per GPU (12.5M = the 100M-row job over 8
     GPUs; weak scaling, rows sharded, no collective).  mlp=bf16: the fused
@@ -546,7 +546,11 @@ def c5_leg(dev, world, rank, rows, reps=3, mlp=torch.bfloat16, check=True):
     def step():
         ops.dfm_forward(X, m.table, wb, Wt, bs, dims, mlp, Wp, bp, out=out)
 
-    step()
+    # warm steps: the first passes after the lighter legs run 5-15 % slower
+    # (clocks ramping: 10.8, 9.9, 9.4, 9.2 ms in one rocprofv3 trace,
+    # profiles/r06_dfm_c5_trace.txt)
+    for _ in range(warm):
+        step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()

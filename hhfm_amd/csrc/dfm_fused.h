@@ -100,6 +100,8 @@ struct BoolC {
 // the 256-row kernel (dfm_wide.hip) at an instantiated shape; false: not
 // instantiated (the caller runs dfm_fused)
 bool dfm_wide_launch(const FusedDfmArgs& a, int TM, int32_t plan, hipStream_t st);
+// bytes of the packed-weight workspace a.packed points to (dfm_fused.hip)
+size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 // base[m] = (Σ_f w·Wp + FM part) + bp into a.fm_out from the pair table
 // C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip; built once per call into a.scratch); false
 // (nothing launched) when it does not fit a.scratch, the rows are too few to

@@ -23,9 +23,9 @@ namespace hhfm {
 // units 4kq..+3 of a tile on lane group kq, exactly the k a lane group
 // supplies next (k order {32s + 4kq .. +3, 32s + 16 + 4kq .. +3}), so no
 // lane movement.  Live: the layer input (104 registers for 32 rows x 416
-// units) + the output being built (104) + 16 (RT = 2; the compiler spills
-// ~56 registers of the prologue's state at the 256 two waves per SIMD
-// leave, measured faster all the same); the
+// units) + the output being built (104) + 16 (RT = 2), within the 256 two
+// waves per SIMD leave: no scratch since the unstaged body moved to its own
+// launch (profiles/r06_kernel_resources.txt); the
 // weight stream per row falls to 2/3 (≈21 B/clk per CU), each 1-KB A
 // fragment feeds three MFMAs.
 //   * weights: dfm_pack_weights_w lays each (layer, 32-unit pass) out as S
@@ -66,10 +66,14 @@ namespace hhfm {
 #ifndef HHFM_WIDE_NWV
 #define HHFM_WIDE_NWV 8
 #endif
-// FM part of staged blocks: the fields' Σ_k Wp_k·e_k² from per-row sums g
-// computed once per staged table row (0: per row and k, as unstaged blocks)
+// FM part of staged blocks: 1 = the fields' Σ_k Wp_k·e_k² from per-row sums g
+// computed once per staged table row; 0 = per row and k, as the overflow
+// launch does.  0: with 1 a row's bits depended on whether its block fitted
+// LDS (the sums are ordered differently), which a batch of mostly grouped rows
+// with a few wide-span blocks showed (tests/test_gpu_dfm.py "mixed").  C5
+// takes its FM part from the pair table (PAIRS) and is not affected.
 #ifndef HHFM_WFM
-#define HHFM_WFM 1
+#define HHFM_WFM 0
 #endif
 // staged blocks: P sums of layer-0 pass t+1 among pass t's MFMA steps (0: at
 // the pass start)
@@ -109,11 +113,13 @@ HHFM_DEV uint32_t relu_bf16x2(uint32_t v) {
   return r;
 }
 
-// one lane-linear 16-B-per-lane LDS-DMA to the LDS byte offset lds_off
-HHFM_DEV void dma16_at(const void* gsrc, uint32_t lds_off) {
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+// one lane-linear 16-B-per-lane LDS-DMA to the LDS byte offset lds_off from
+// the uniform base + the lane's 32-bit byte offset (SGPR base: no 64-bit
+// per-lane address registers, which the staged kernel has none spare for)
+HHFM_DEV void dma16_at(const void* base, uint32_t voff, uint32_t lds_off) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
                :
-               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds_off))
+               : "v"(voff), "s"(base), "s"(__builtin_amdgcn_readfirstlane(lds_off))
                : "memory");
 }
 
@@ -122,7 +128,9 @@ HHFM_DEV void dma16_at(const void* gsrc, uint32_t lds_off) {
 //   layer i: W_i[32t + 16j + r][32s + 4kq .. +3] ++ W_i[..][32s + 16 + 4kq .. +3]
 // zero outside the layer's rows / columns
 __global__ __launch_bounds__(256) void dfm_pack_weights_w(FusedDfmArgs a, int TM, int S0,
-                                                          uint4* __restrict__ out) {
+                                                          uint4* __restrict__ out,
+                                                          uint32_t* __restrict__ ovf) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ovf = 0;   // the overflow count (dfm_fused_w)
   const int64_t n0 = (int64_t)TM * S0 * 2;            // layer-0 1-KB units
   const int64_t total = (n0 + 2 * (int64_t)TM * TM * 2) * 64;
   const int fe0 = (int)(a.perm & 15);   // caller field of internal field 0 (the item)
@@ -167,10 +175,20 @@ __global__ __launch_bounds__(256) void dfm_pack_weights_w(FusedDfmArgs a, int TM
   }
 }
 
-// RT row tiles (16 rows) per wave, NWV waves: 3 x 4 (one wave per SIMD,
-// 192 rows) or 2 x 8 (two waves per SIMD, 256 rows)
-template <int TM, int S0, int NF, bool PAIRS, int RT = 3, int NWV = 4>
-__global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
+// Overflow list, in the packed-weight workspace past the weights: the count
+// in a 256-B head, then row-unit indices (units of the overflow launch's rows)
+constexpr int kOvfHead = 64;
+
+// One block of kWideRows rows from row m0.  RT row tiles (16 rows) per wave,
+// NWV waves: 3 x 4 (one wave per SIMD, 192 rows) or 2 x 8 (two waves per
+// SIMD, 256 rows).  OVF false: the staged body only — a block whose id spans
+// do not fit LDS appends its ovf_rows-row units to the overflow list and
+// ends; OVF true: the unstaged body (P and table rows read from memory), for
+// the listed units.  Each kernel then holds one body: the staged kernel at
+// two waves per SIMD has no registers left for the unstaged one's state
+// (224 B of scratch per lane when both were compiled together).
+template <int TM, int S0, int NF, bool PAIRS, int RT, int NWV, bool OVF>
+HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, int ovf_rows) {
   constexpr int kWideRows = NWV * 16 * RT;
   constexpr int NTH = NWV * 64;
   // PAIRS: a.fmbase[m] = (Σ_f w·Wp + FM part) + bp from the pair table
@@ -205,7 +223,6 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
   const int tid = threadIdx.x, l = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = l & 15, kq = l >> 4;
-  const int64_t m0 = (int64_t)blockIdx.x * kWideRows;
   const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   const int k = a.k;
   const float* P = reinterpret_cast<const float*>(a.proj);
@@ -233,7 +250,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
   auto cunits = [](int c) { return c < TM ? 2 * S0 : 2 * TM; };
   auto cbase = [](int c) { return c < TM ? c * 2 * S0 : TM * 2 * S0 + (c - TM) * 2 * TM; };
   auto dma_unit = [&](int c, int u) {
-    dma16_at(a.packed + (int64_t)(cbase(c) + u) * 64 + l, lds0 + (c % 3) * kSlotB + u * 1024);
+    dma16_at(a.packed + (int64_t)(cbase(c) + u) * 64, 16 * l, lds0 + (c % 3) * kSlotB + u * 1024);
   };
   for (int c = 0; c < 2; ++c)
     for (int u = wv; u < cunits(c); u += NWV) dma_unit(c, u);
@@ -259,7 +276,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       if (f < F) y1 += wv8[f] * wpl[f];
     ylds[tid] = y1;
   }
-  for (int x = tid; x < kWideRows * NF; x += NTH) {
+  for (int x = tid; x < (OVF ? 0 : kWideRows * NF); x += NTH) {
     const int row = x / NF, f = 1 + x % NF;
     atomicMin(&plo[f], ids[row * F + f]);
     atomicMax(&plo[kFusedMaxF + f], ids[row * F + f]);
@@ -267,15 +284,15 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
   __syncthreads();
   // all projected fields' P rows and table rows lo..hi staged in LDS when
   // they fit (rows grouped by user: the user's and the contexts' few rows);
-  // otherwise the block reads them from memory.  The body is compiled once
-  // per case: a uniform branch per field between LDS and memory reads is
-  // merged by the compiler into flat loads.
+  // otherwise the block's units go to the overflow launch, which reads them
+  // from memory.  (One kernel with both bodies behind a uniform branch per
+  // field between LDS and memory reads was merged by the compiler into flat
+  // loads, and one with both bodies behind one branch spilled.)
   const int ek = k / 2;   // bf16 table row in floats
   // staged table rows 16 B apart in bank space (a row is 0 mod 64 banks), so
   // the FM part's reads of different rows by one lane group do not conflict
   const int ekp = PAIRS ? 0 : ek + 4;
-  bool allfit;
-  {
+  if constexpr (!OVF) {
     int used = 0;
     for (int f = 1; f < F; ++f) {
       const int span = plo[kFusedMaxF + f] - plo[f] + 1;
@@ -286,9 +303,19 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       }
       used += span * (kPsLd + ekp) + (PAIRS ? 0 : ((span + 3) & ~3));
     }
-    allfit = used <= kPsFloats;
+    if (used > kPsFloats || (HHFM_WKO & 32)) {   // uniform: every thread read the same plo
+      if (tid == 0) {
+        const int64_t u0 = m0 / ovf_rows;
+        int n = 0;
+        for (int64_t r = m0; r < m0 + kWideRows && r < a.B; r += ovf_rows) ++n;
+        const uint32_t at = atomicAdd(ovf, (uint32_t)n);
+        for (int j = 0; j < n; ++j) ovf[kOvfHead + at + j] = (uint32_t)(u0 + j);
+      }
+      dma_wait();   // passes 0 and 1 landed before the workgroup's LDS is released
+      return;
+    }
   }
-  if (allfit && !(HHFM_WKO & 32)) {
+  if constexpr (!OVF) {
     int used = 0;
     for (int f = 1; f < F; ++f) {
       const int lo = plo[f], span = plo[kFusedMaxF + f] - lo + 1;
@@ -344,7 +371,11 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       for (int f = 1; f < F; ++f) pid[rt][f] = ids[(row0 + 16 * rt) * F + f];
     // staged blocks: LDS float offsets of the rows' P and table rows, and
     // ½ Σ_f g[x_f] of the rows (lane group 0 adds it at the end)
-    int pb[RT][F], eb[RT][F];
+    // (offsets < 40,960 floats: two 16-bit offsets per register, unpacked
+    // at each use by volatile asm so the unpacked values are not kept live —
+    // the staged kernel runs layer 0 at its 256-register limit)
+    static_assert(kPsFloats < 65536, "wide DeepFM kernel: 16-bit LDS offsets");
+    uint32_t pbw[(RT + 1) / 2][F] = {}, ebw[(RT + 1) / 2][F] = {};
     float gh[RT] = {};
     if constexpr (ST) {
 #pragma unroll
@@ -353,12 +384,22 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
         const int gofs = plo[4 * kFusedMaxF + f];
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
-          pb[rt][f] = pofs + (pid[rt][f] - lo) * kPsLd;
-          eb[rt][f] = eofs + (pid[rt][f] - lo) * ekp;
+          pbw[rt >> 1][f] |= (uint32_t)(pofs + (pid[rt][f] - lo) * kPsLd) << (16 * (rt & 1));
+          ebw[rt >> 1][f] |= (uint32_t)(eofs + (pid[rt][f] - lo) * ekp) << (16 * (rt & 1));
           if constexpr (HHFM_WFM && !PAIRS) gh[rt] += pst[gofs + pid[rt][f] - lo];
         }
       }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) pin(gh[rt]);   // summed here, not at the store
     }
+    auto half16 = [](uint32_t w, int hi) -> int {
+      uint32_t o;
+      if (hi) asm volatile("v_lshrrev_b32 %0, 16, %1" : "=v"(o) : "v"(w));
+      else asm volatile("v_and_b32 %0, 0xffff, %1" : "=v"(o) : "v"(w));
+      return (int)o;
+    };
+    auto pbo = [&](int rt, int f) { return half16(pbw[rt >> 1][f], rt & 1); };
+    auto ebo = [&](int rt, int f) { return half16(ebw[rt >> 1][f], rt & 1); };
 
     // FM second-order part (DFM.py:114-122) before layer 0: per k32 step,
     // the item's 8 columns 32s + 8kq .. +7 from its B operand, the other
@@ -383,7 +424,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
           uint4 u;
           if constexpr (ST)
             u = *reinterpret_cast<const uint4*>(
-                reinterpret_cast<const uint16_t*>(pst + eb[rt][f2]) + 32 * s + 8 * kq);
+                reinterpret_cast<const uint16_t*>(pst + ebo(rt, f2)) + 32 * s + 8 * kq);
           else
             u = *reinterpret_cast<const uint4*>(E + (int64_t)pid[rt][f2] * k + 32 * s + 8 * kq);
           const uint32_t u4[4] = {u.x, u.y, u.z, u.w};
@@ -424,7 +465,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
         for (int rt = 0; rt < RT; ++rt) {
           const float* pp;
           if constexpr (ST)
-            pp = pst + pb[rt][f] + pos0;
+            pp = pst + pbo(rt, f) + pos0;
           else
             pp = P + (f - 1) * a.proj_fstride + (int64_t)pid[rt][f] * a.proj_ld + pos0;
 #pragma unroll
@@ -449,7 +490,7 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       for (int u = 0; u < kPU; ++u) {
         if (u < s * kPU / S0 || u >= (s + 1) * kPU / S0) continue;
         const int f = 1 + u / RT, rt = u % RT;
-        const float* pp = pst + pb[rt][f] + pos0;
+        const float* pp = pst + pbo(rt, f) + pos0;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const float4 x = *reinterpret_cast<const float4*>(pp + 8 * j);
@@ -596,6 +637,10 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       }
     });
 
+    // the lane index formed again here (volatile: not kept live from the
+    // prologue — at two waves per SIMD the staged kernel has no register for it)
+    int le;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(le));
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       float pt = part[rt], yy = y2[rt];
@@ -603,33 +648,79 @@ __global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a) {
       pt += __shfl_xor(pt, 32, kWave);
       yy += __shfl_xor(yy, 16, kWave);
       yy += __shfl_xor(yy, 32, kWave);
-      const int row = row0 + 16 * rt;
+      const int row = 16 * RT * wv + (le & 15) + 16 * rt;
       const int64_t m = m0 + row;
       if constexpr (ST && HHFM_WFM && !PAIRS) yy -= 0.5f * gh[rt];   // − ½ Σ_f g[x_f], staged fields
-      if (kq == 0 && m < a.B) {
+      if (le < 16 && m < a.B) {
         if constexpr (PAIRS) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + pt;
         else a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
       }
     }
   };
-  if (allfit) body(BoolC<true>{});
-  else body(BoolC<false>{});
+  body(BoolC<!OVF>{});
+}
+
+template <int TM, int S0, int NF, bool PAIRS, int RT = 3, int NWV = 4, bool OVF = false>
+__global__ __launch_bounds__(NWV * 64, 1) void dfm_fused_w(FusedDfmArgs a, uint32_t* ovf,
+                                                           int ovf_rows) {
+  constexpr int kWideRows = NWV * 16 * RT;
+  if constexpr (!OVF) {
+    wide_rows<TM, S0, NF, PAIRS, RT, NWV, false>(a, (int64_t)blockIdx.x * kWideRows, ovf,
+                                                 ovf_rows);
+  } else {   // grid-stride over the listed units (kWideRows == ovf_rows)
+    const uint32_t n = ovf[0];
+    for (uint32_t u = blockIdx.x; u < n; u += gridDim.x) {
+      __syncthreads();   // the previous unit's LDS reads are done before it is refilled
+      wide_rows<TM, S0, NF, PAIRS, RT, NWV, true>(a, (int64_t)ovf[kOvfHead + u] * kWideRows,
+                                                  ovf, ovf_rows);
+    }
+  }
+}
+
+// the staged launch, then the overflow launch over the units it listed:
+// 4 waves x ORT row tiles (one wave per SIMD), a unit a divisor of the
+// staged block; at most one workgroup per CU (the LDS), grid-stride
+template <int T, int A, int N, bool PAIRS, int RT, int NWV>
+static void wide_launch_rows(const FusedDfmArgs& c, uint32_t* ovf, bool first, hipStream_t st) {
+  constexpr int kRowsWG = NWV * 16 * RT;
+  constexpr int ORT = kRowsWG % 128 == 0 ? 2 : 1, kRowsOvf = 64 * ORT;
+  const int64_t g1 = (c.B + kRowsWG - 1) / kRowsWG, g2 = (c.B + kRowsOvf - 1) / kRowsOvf;
+  if (!first) (void)hipMemsetAsync(ovf, 0, sizeof(uint32_t), st);   // (the packing zeroed it)
+  hipLaunchKernelGGL((dfm_fused_w<T, A, N, PAIRS, RT, NWV, false>), dim3((unsigned)g1),
+                     dim3(NWV * 64), 0, st, c, ovf, kRowsOvf);
+  hipLaunchKernelGGL((dfm_fused_w<T, A, N, PAIRS, ORT, 4, true>),
+                     dim3((unsigned)(g2 < 256 ? g2 : 256)), dim3(256), 0, st, c, ovf, kRowsOvf);
 }
 
 template <int T, int A, int N, int RT, int NWV>
 static void wide_launch_shape(const FusedDfmArgs& a, hipStream_t st) {
   constexpr int kRowsWG = NWV * 16 * RT;
-  const dim3 grid((unsigned)((a.B + kRowsWG - 1) / kRowsWG));
   const int64_t units = ((int64_t)T * A * 2 + 2 * (int64_t)T * T * 2) * 64;
   const int pblocks = (int)((units + 255) / 256 < 2048 ? (units + 255) / 256 : 2048);
+  // the overflow list after the packed weights, in the rest of the packed
+  // workspace (dfm_fused_pack_bytes: ~6.6 MB at C5); rows in chunks whose
+  // units always fit it (one chunk below ~200 M rows)
+  const size_t wbytes = ((size_t)units * 16 + 255) & ~size_t(255);
+  uint32_t* ovf = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(const_cast<uint4*>(a.packed)) +
+                                              wbytes);
   hipLaunchKernelGGL(dfm_pack_weights_w, dim3(pblocks), dim3(256), 0, st, a, T, A,
-                     const_cast<uint4*>(a.packed));
-  if (dfm_fm_pairs(a, true, st)) {
-    FusedDfmArgs b = a;
-    b.fmbase = a.fm_out;
-    hipLaunchKernelGGL((dfm_fused_w<T, A, N, true, RT, NWV>), grid, dim3(NWV * 64), 0, st, b);
-  } else {
-    hipLaunchKernelGGL((dfm_fused_w<T, A, N, false, RT, NWV>), grid, dim3(NWV * 64), 0, st, a);
+                     const_cast<uint4*>(a.packed), ovf);
+  const int64_t cap = ((int64_t)dfm_fused_pack_bytes(a.L, a.dims, true) - (int64_t)wbytes) / 4 -
+                      kOvfHead;
+  const int64_t chunk = cap / (kRowsWG / 64) * kRowsWG;   // units of >= 64 rows
+  const bool pairs = dfm_fm_pairs(a, true, st);
+  for (int64_t r0 = 0; r0 < a.B; r0 += chunk) {
+    FusedDfmArgs c = a;
+    c.B = a.B - r0 < chunk ? a.B - r0 : chunk;
+    c.idx += r0 * a.F;
+    if (c.order) c.order += r0;   // out[order[m]]: order holds the caller's rows
+    else c.out += r0;
+    if (pairs) {
+      c.fmbase = a.fm_out + r0;
+      wide_launch_rows<T, A, N, true, RT, NWV>(c, ovf, r0 == 0, st);
+    } else {
+      wide_launch_rows<T, A, N, false, RT, NWV>(c, ovf, r0 == 0, st);
+    }
   }
 }
 

@@ -412,14 +412,18 @@ def test_topk_dense_split_waves(B, N):
                                                 (64, [150, 150, 150], 20000, True),
                                                 (64, [150, 150, 150], 777, False),
                                                 (64, [150, 150, 150], 90001, True),
-                                                (256, [400, 400, 400], 81000, False)])
+                                                (256, [400, 400, 400], 81000, False),
+                                                (64, [150, 150, 150], 20000, "mixed"),
+                                                (256, [400, 400, 400], 82000, "mixed")])
 def test_dfm_wide_item(k, layers, B, grouped):
     """The wide ITEM kernel (dfm_wide.hip, 256 rows per workgroup; shapes it is instantiated for:
     F = 5 with k = 256 / 3 x 400 — C5 — and k = 64 / 3 x 150): against the
     bf16-rounding oracle (5e-3 of the magnitude) and the 128-row kernel
     (PLAN_NARROW), with rows grouped by user (blocks stage their P and table
     rows in LDS) and with random ids (blocks read them from memory, B not a
-    multiple of 256); a row's score never depends on its block.  B >= 16 x
+    multiple of 256) — those blocks run in the overflow launch — and mixed
+    (grouped, a few rows with random context ids: most blocks staged, some in
+    the overflow launch); a row's score never depends on its block.  B >= 16 x
     the table's 5,051 rows (the last two cases) takes the FM part from the
     pair table (dfm_wide PAIRS, the default C5 kernel), else from the rows;
     the FM-rows variant (PLAN_ROW_FM) is compared there too."""
@@ -435,6 +439,9 @@ def test_dfm_wide_item(k, layers, B, grouped):
         cols.append(rng.integers(off, off + c, B) if grouped else rng.integers(0, M, B))
         off += c
     X = np.stack(cols, 1).astype(np.int32)
+    if grouped == "mixed":
+        wild = rng.random(B) < 0.002
+        X[wild, 2:] = rng.integers(0, M, (int(wild.sum()), 3))
     W = m.get_weights()
     Ls = [W[f"layer_{i}"] for i in range(3)]
     Bs = [W[f"bias_{i}"] for i in range(3)]
