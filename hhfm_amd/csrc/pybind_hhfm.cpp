@@ -183,6 +183,14 @@ PYBIND11_MODULE(_hhfm, m) {
     return n;
   });
 
+  m.def("sample_negative_workspace_ex", [](int64_t B, int num, int64_t lo, int64_t hi,
+                                          int64_t nkeys) {
+    size_t n = 0;
+    check(hhfm_sample_negative_workspace_ex(B, num, lo, hi, nkeys, &n),
+          "hhfm_sample_negative_workspace_ex");
+    return n;
+  });
+
   m.def("sample_negative",
         [](uptr state, int64_t lo, int64_t hi, uptr rows, int64_t B, int ncols, int item_col,
            int num, uptr keys, int64_t nkeys, uptr codes, int64_t ncodes, uptr samples, uptr ws,

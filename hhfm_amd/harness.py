@@ -65,6 +65,12 @@ class _PairSet:
         return hit
 
 
+# the device sampler's re-draw membership test: per-key bitmaps (True) or the
+# binary searches over the sorted codes (False: the workspace without bitmaps);
+# identical results — the switch exists for tests
+SAMPLER_BITMAPS = True
+
+
 class DevicePairSet:
     """positive_feedback as the two sorted device arrays hhfm_pf_contains
     searches: distinct keys [nkeys, key_cols] int32 in lexicographic order,
@@ -198,13 +204,12 @@ class Train(object):
         B, ncols = data.shape
         pairs = self._device_pairs(dev, ncols - 1)
         nat = native()
-        nbytes = nat.sample_negative_workspace(B, num)
+        nbytes = (nat.sample_negative_workspace_ex(B, num, lo, hi, pairs.n) if SAMPLER_BITMAPS
+                  else nat.sample_negative_workspace(B, num))
         cache = getattr(self, "_sampler_bufs", None)
-        if cache is None or cache["dev"] != dev or cache["ws"].numel() < nbytes or \
-                cache["host"].numel() < B * num:
+        if cache is None or cache["dev"] != dev or cache["ws"].numel() < nbytes:
             cache = self._sampler_bufs = {
                 "dev": dev, "ws": torch.empty(nbytes, dtype=torch.uint8, device=dev),
-                "host": torch.empty(B * num, dtype=torch.int64, pin_memory=True),
                 "state": torch.empty(625, dtype=torch.int32, pin_memory=True)}
         sd = torch.from_numpy(state.view(np.int32)).to(dev)
         rows = torch.from_numpy(np.ascontiguousarray(data, dtype=np.int32)).to(dev)
@@ -212,15 +217,17 @@ class Train(object):
         nat.sample_negative(sd.data_ptr(), lo, hi, rows.data_ptr(), B, ncols, 1, num,
                             pairs.keys.data_ptr() if pairs.n else 0, pairs.n,
                             pairs.codes.data_ptr() if pairs.n else 0, pairs.codes.numel(),
-                            out.data_ptr(), cache["ws"].data_ptr(), cache["ws"].numel(),
+                            out.data_ptr(), cache["ws"].data_ptr(), nbytes,
                             ops._stream(dev))
-        host, hstate = cache["host"][:B * num], cache["state"]
+        # the samples land in a pinned block of torch's caching host allocator
+        # that the returned array owns (no second host copy of B x num int64)
+        host, hstate = torch.empty(B * num, dtype=torch.int64, pin_memory=True), cache["state"]
         host.copy_(out, non_blocking=True)
         hstate.copy_(sd, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
         new = hstate.numpy().view(np.uint32)
         np.random.set_state((st[0], new[:624].copy(), int(new[624]), st[3], st[4]))
-        return host.numpy().reshape(B, num).copy()
+        return host.numpy().reshape(B, num)
 
     # -- H4 -----------------------------------------------------------------
     def evaluate_AUC(self, data1):

@@ -507,6 +507,12 @@ int hhfm_topk_walk(const int32_t* pred, int64_t B, int32_t P, const int32_t* tar
  * hhfm_sample_negative_workspace(B, num) bytes, no initialisation needed.
  * Replaces FM.py:284-294 (and OurModel7.py, AFM.py, DFM.py's copies). */
 int hhfm_sample_negative_workspace(int64_t B, int32_t num, size_t* ws_bytes);
+/* The same, sized for the faster re-draw test: per-key bitmaps of the
+ * positives over [lo, hi) (nkeys x ceil((hi - lo) / 32) words, used when at
+ * most 256 MB); hhfm_sample_negative takes the bitmap path whenever ws_bytes
+ * covers it.  Results are identical either way. */
+int hhfm_sample_negative_workspace_ex(int64_t B, int32_t num, int64_t lo, int64_t hi,
+                                      int64_t nkeys, size_t* ws_bytes);
 int hhfm_sample_negative(uint32_t* mt_state, int64_t lo, int64_t hi, const int32_t* rows,
                          int64_t B, int32_t ncols, int32_t item_col, int32_t num,
                          const int32_t* keys, int64_t nkeys, const int64_t* codes,

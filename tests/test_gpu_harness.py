@@ -184,14 +184,17 @@ class _PF:
         self.positive_feedback, self.n_user, self.n_item = pf, n_user, n_item
 
 
+@pytest.mark.parametrize("bitmaps", [True, False])
 @pytest.mark.parametrize("n_item,cover", [(5, 0.8), (2, 0.5), (64, 0.9), (65, 0.5),
                                           (1000, 0.97), (1, 0.0)])
-def test_sample_negative_on_device_heavy_rejection(n_item, cover):
+def test_sample_negative_on_device_heavy_rejection(n_item, cover, bitmaps, monkeypatch):
     """Keys whose positives cover most of the catalog force long re-draw
     chains (several rounds of 256 entries, values running out, generation
     rounds that slide the MT window); catalogs of 2^k and 2^k + 1 items set
     the mask's rejection rate to 0 and ~1/2; one item draws nothing
-    (randint(lo, lo + 1)).  Device == host harness, samples and state."""
+    (randint(lo, lo + 1)).  Device == host harness, samples and state, with
+    the re-draw test on key bitmaps and on the binary searches."""
+    monkeypatch.setattr(harness, "SAMPLER_BITMAPS", bitmaps)
     rng = np.random.default_rng(n_item)
     n_user, ncols = 40, 4
     keys = [tuple(int(v) for v in rng.integers(0, 50, ncols - 1)) for _ in range(60)]
@@ -221,3 +224,25 @@ def test_sample_negative_on_device_refuses_a_hang():
                          model=DeviceOracleModel(None, None, n_user, n_item))
     with pytest.raises(ValueError):
         devt.sample_negative(X, 3)
+
+
+def test_sample_negative_on_device_one_free_item_in_50k():
+    """Keys whose positives cover all but ONE item of a 50,000-item catalog:
+    every entry of such a row re-draws ~50,000 times (the reference finishes,
+    slowly), far past the old guard of 64 + count/1024 generation rounds.
+    Device == host harness, samples and state."""
+    n_user, n_item = 10, 50_000
+    rng = np.random.default_rng(50_000)
+    pf = {}
+    for key in ((1, 2, 3), (4, 5, 6)):
+        free = int(rng.integers(0, n_item))
+        pf[key] = set(n_user + i for i in range(n_item) if i != free)
+    rows = [[1, n_user, 2, 3]] * 6 + [[4, n_user, 5, 6]] * 6 + [[7, n_user, 8, 9]] * 4
+    X = np.asarray(rows, dtype=np.int64)
+    data = _PF(pf, n_user, n_item)
+    host = harness.Train(data=data, model=None)
+    devt = harness.Train(data=data, model=DeviceOracleModel(None, None, n_user, n_item))
+    a = _both(host, devt, X, 2, lambda: np.random.seed(11))
+    for key, r in ((1, a[:6]), (4, a[6:12])):
+        k = (key, key + 1, key + 2)
+        assert not any(int(v) in pf[k] for v in r.ravel())
