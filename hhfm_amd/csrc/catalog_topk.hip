@@ -526,6 +526,9 @@ __global__ __launch_bounds__(256) void catalog_main(
 #ifndef HHFM_RING_TIMING
 #define HHFM_RING_TIMING 0   // diagnostic build: per-phase s_memtime sums (hhfm_debug_ring_timing)
 #endif
+#if (HHFM_MAIN_KO || HHFM_RING_KO || HHFM_RING_TIMING) && !defined(HHFM_DIAG_BUILD)
+#error "K2 knock-out / timing macros give wrong results: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
 #if HHFM_RING_TIMING
 // [0] publish (vmcnt + barrier + staging issue), [1] MFMA chain to ballots,
 // [2] selection, [3] wave-tiles, [4] whole kernel per wave, [5] waves

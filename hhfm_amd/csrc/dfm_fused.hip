@@ -49,6 +49,10 @@
 #include "dfm_fused.h"
 
 
+#if (defined(HHFM_KO_PROJP) || defined(HHFM_KO_PROJFM)) && !defined(HHFM_DIAG_BUILD)
+#error "HHFM_KO_PROJP / HHFM_KO_PROJFM give wrong results: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
+
 namespace hhfm {
 
 

@@ -48,6 +48,9 @@ namespace hhfm {
 #ifndef HHFM_WKO
 #define HHFM_WKO 0
 #endif
+#if HHFM_WKO && !defined(HHFM_DIAG_BUILD)
+#error "HHFM_WKO knock-outs give wrong results: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
 // 16-row tiles per wave and waves per workgroup: 2 x 8 = 256 rows, two waves
 // per SIMD (C5 bf16 10.0-10.3 ms, bit-identical), against 3 x 4 = 192 rows at
 // one wave per SIMD (12.9-13.0 ms; profiles/r04_k3w_two_waves_ab.txt): the
