@@ -23,22 +23,6 @@
 
 namespace hhfm {
 
-// CUs of the device that owns `st` (the stream's device, not the calling
-// thread's current one), cached per device: the persistent grids ask per call
-static int stream_cu_count(hipStream_t st) {
-  static std::atomic<int> cache[64];
-  int dev = 0;
-  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
-  if (dev < 0 || dev >= 64) return 256;
-  int c = cache[dev].load(std::memory_order_relaxed);
-  if (c <= 0) {
-    c = 256;
-    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
-    cache[dev].store(c, std::memory_order_relaxed);
-  }
-  return c;
-}
-
 static size_t a256(size_t x) { return (x + 255) & ~size_t(255); }
 
 HHFM_DEV float tab(const void* E, int bf16, int64_t id, int k, int c) {

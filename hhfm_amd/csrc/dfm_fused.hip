@@ -55,6 +55,22 @@
 
 namespace hhfm {
 
+#ifndef HHFM_F32S_TIMING
+#define HHFM_F32S_TIMING 0   // diagnostic build: dfm_fused_f32s per-phase s_memtime sums
+#endif
+#if HHFM_F32S_TIMING && !defined(HHFM_DIAG_BUILD)
+#error "HHFM_F32S_TIMING: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
+#if HHFM_F32S_TIMING
+// per wave and block: [0] ids + plan loads, [1] item gather issue + spans +
+// staging, [2] layer-0 adds, [3] hidden layers, [4] epilogue, [5] blocks x waves
+// (scripts/diag/f32s_phases.py)
+__device__ unsigned long long g_f32s_t[8];
+#define HHFM_F32S_T(x) x
+#else
+#define HHFM_F32S_T(x)
+#endif
+
 
 constexpr int kFusedRows = 128;   // rows per workgroup (4 waves x 32)
 
@@ -983,6 +999,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   const int64_t m0 = (int64_t)blockIdx.x * Cfg::kRows;
   const int F = a.F, k = a.k, L = a.L;
   const int H = (L - 1) * TM * 2;            // hidden half-chunks
+  HHFM_F32S_T(uint64_t tq[6]; tq[0] = __builtin_amdgcn_s_memtime();)
 
   for (int x = tid; x < Cfg::kRows * F; x += NT) {
     const int64_t m = m0 + x / F;
@@ -996,6 +1013,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     phi[tid] = -1;
   }
   __syncthreads();
+  HHFM_F32S_T(tq[1] = __builtin_amdgcn_s_memtime();)
   const int myrow = 16 * wv + r;
   f32x4 X[T16];
   // field 1 (the item: its ids span the whole catalog, it is never staged)
@@ -1078,6 +1096,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     dma_half(0, 0);
     dma_half(1, 1);
   }
+  HHFM_F32S_T(tq[2] = __builtin_amdgcn_s_memtime();)
 
   // ----- layer 0 from P: X = Σ_f P_f[x_f] (lane group kq: units 16t+4kq..+3),
   // straight into the registers of layer 1's input -----
@@ -1111,6 +1130,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     }
   }
   // ----- hidden layers: 6 split-bf16 MFMAs per tile and 32-k step -----
+  HHFM_F32S_T(asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); tq[3] = __builtin_amdgcn_s_memtime();)
   auto mma = [](const bf16x8& w, const bf16x8& x, const f32x4& c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, x, c, 0, 0, 0);
   };
@@ -1189,6 +1209,7 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
     }
   }
   dma_wait();   // the trailing (re-read) DMAs
+  HHFM_F32S_T(tq[4] = __builtin_amdgcn_s_memtime();)
 
   const float* blL = blv + (L - 1) * NR;
   float part = 0.f;
@@ -1203,6 +1224,14 @@ __global__ __launch_bounds__(NW * 64, 1) void dfm_fused_f32s(FusedDfmArgs a) {
   part += __shfl_xor(part, 32, kWave);
   const int64_t m = m0 + myrow;
   if (kq == 0 && m < a.B) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + part;
+#if HHFM_F32S_TIMING
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tq[5] = __builtin_amdgcn_s_memtime();
+  if (l == 0) {
+    for (int q = 0; q < 5; ++q) atomicAdd(&g_f32s_t[q], tq[q + 1] - tq[q]);
+    atomicAdd(&g_f32s_t[5], 1ull);
+  }
+#endif
 }
 
 // the FM part's per-element steps, spelled out (fused or not) so the two
@@ -1981,3 +2010,13 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
 }
 
 }  // namespace hhfm
+
+#if HHFM_F32S_TIMING
+extern "C" int hhfm_debug_f32s_timing(unsigned long long* out) {
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hhfm::g_f32s_t), sizeof(hhfm::g_f32s_t)) != hipSuccess)
+    return -1;
+  static const unsigned long long zero[8] = {0};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(hhfm::g_f32s_t), zero, sizeof(zero));
+}
+#endif

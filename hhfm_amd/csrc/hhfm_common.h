@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/hhfm.h"
 
 #define HHFM_DEV __device__ __forceinline__
@@ -91,6 +93,22 @@ HHFM_DEV float group_sum(float x) {
 #pragma unroll
   for (int m = G / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, kWave);
   return x;
+}
+
+// CUs of the device that owns `st` (the stream's device, not the calling
+// thread's current one), cached per device: the persistent grids ask per call
+inline int stream_cu_count(hipStream_t st) {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= 64) return 256;
+  int c = cache[dev].load(std::memory_order_relaxed);
+  if (c <= 0) {
+    c = 256;
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    cache[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
 }
 
 }  // namespace hhfm
