@@ -51,6 +51,15 @@ namespace hhfm {
 #if HHFM_FUSED_TIMING && !defined(HHFM_DIAG_BUILD)
 #error "HHFM_FUSED_TIMING: diagnostic builds only (-DHHFM_DIAG_BUILD)"
 #endif
+// diagnostic knock-outs of the in-kernel merge (wrong results; timing only):
+// 1 the last arriver merges zero keys instead of loading the S lists, 2 it
+// does not merge at all
+#ifndef HHFM_FUSED_KO
+#define HHFM_FUSED_KO 0
+#endif
+#if HHFM_FUSED_KO && !defined(HHFM_DIAG_BUILD)
+#error "HHFM_FUSED_KO: diagnostic builds only (-DHHFM_DIAG_BUILD)"
+#endif
 #if HHFM_FUSED_TIMING
 // per workgroup, wave 0's s_memtime at kFusedMarks points (plain stores: no
 // atomics that would queue beside the hand-off); host side: differences
@@ -882,7 +891,7 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
     HHFM_MARK(19);
     lds_barrier();
     HHFM_MARK(20);
-    merged = last_sh != 0;   // uniform
+    merged = last_sh != 0 && !(HHFM_FUSED_KO & 2);   // uniform
     if (merged) {
       // no instruction: keeps the sc1 loads below the barrier
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -911,7 +920,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
 #pragma unroll
           for (int x = 0; x < 2; ++x) {
             const int sl = 2 * x + h;
-            v[u][x] = __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[u][x] = (HHFM_FUSED_KO & 1) ? 0ull
+                      : __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             v[u][x] = sl < S ? v[u][x] : 0ull;
           }
 #pragma unroll
