@@ -53,7 +53,7 @@ namespace hhfm {
 #endif
 // diagnostic knock-outs of the in-kernel merge (wrong results; timing only):
 // 1 the last arriver merges zero keys instead of loading the S lists, 2 it
-// does not merge at all
+// does not merge at all, 4 it merges but writes no output
 #ifndef HHFM_FUSED_KO
 #define HHFM_FUSED_KO 0
 #endif
@@ -900,36 +900,68 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
       // queries; up to 4 lists per query every load is issued before any
       // merge (one memory latency; merged from registers — a rolled merge
       // staged through LDS measured 60 % slower), more take a rolled loop
+      // (src: lane j's rank of list sl of the wave's query u)
       auto src = [&](int u, int sl) {
         return (const gu64*)(part + ((((int64_t)g * S + (sl < S ? sl : 0)) * kQPerWave +
                                       wv * QW + u) << 5) + j);
       };
-      auto finish = [&](int u, uint64_t a) {
-        merge_keys<32>(a, xor_lane64(a, 32));   // the odd lists' half into the even's
+      auto store = [&](int u, uint64_t a) {
         const int64_t b = q0 + wv * QW + u;
-        if (b < B && l < K) {
+        if (b < B && l < K && !((HHFM_FUSED_KO & 4) && a != 1ull)) {
           out_s[b * K + l] = ukey_inv((uint32_t)(a >> 32));
           const int32_t it = ~(int32_t)(uint32_t)a;
           out_i[b * K + l] = it == kNoIdx ? kNoIdx : it + gbase;
         }
       };
       if (S <= 4) {
-        uint64_t v[QW][2];
+        // half h merges lists h and h + 2: the second loaded reversed (lane
+        // j takes rank 31 - j), so max(first, second) is bitonic without a
+        // lane permutation; half 0 sorts it descending, half 1 ascending, so
+        // the final max(half 0, half 1 swapped) is bitonic too.  The QW
+        // queries' networks run stage by stage (their chains interleave).
+        uint64_t a[QW];
 #pragma unroll
-        for (int u = 0; u < QW; ++u)
+        for (int u = 0; u < QW; ++u) {
+          uint64_t v[2];
 #pragma unroll
           for (int x = 0; x < 2; ++x) {
             const int sl = 2 * x + h;
-            v[u][x] = (HHFM_FUSED_KO & 1) ? 0ull
-                      : __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            v[u][x] = sl < S ? v[u][x] : 0ull;
+            const gu64* q = src(u, sl) + (x == 1 ? 31 - 2 * j : 0);
+            v[x] = (HHFM_FUSED_KO & 1) ? 0ull
+                   : __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[x] = sl < S ? v[x] : 0ull;
           }
-#pragma unroll
-        for (int u = 0; u < QW; ++u) {
-          uint64_t a = v[u][0];
-          if (S > 2) merge_keys<32>(a, v[u][1]);
-          finish(u, a);
+          a[u] = v[1] > v[0] ? v[1] : v[0];
         }
+        const bool asc = h != 0;
+#pragma unroll
+        for (int d = 16; d >= 1; d >>= 1) {
+          const bool keep_max = ((j & d) == 0) != asc;
+          uint64_t p[QW];
+#pragma unroll
+          for (int u = 0; u < QW; ++u) p[u] = xor_lane64(a[u], d);
+#pragma unroll
+          for (int u = 0; u < QW; ++u) a[u] = ((p[u] > a[u]) == keep_max) ? p[u] : a[u];
+        }
+        // half 0: max with half 1's ascending list, then a descending cleanup
+        {
+          uint64_t p[QW];
+#pragma unroll
+          for (int u = 0; u < QW; ++u) p[u] = xor_lane64(a[u], 32);
+#pragma unroll
+          for (int u = 0; u < QW; ++u) a[u] = p[u] > a[u] ? p[u] : a[u];
+        }
+#pragma unroll
+        for (int d = 16; d >= 1; d >>= 1) {
+          const bool keep_max = (j & d) == 0;
+          uint64_t p[QW];
+#pragma unroll
+          for (int u = 0; u < QW; ++u) p[u] = xor_lane64(a[u], d);
+#pragma unroll
+          for (int u = 0; u < QW; ++u) a[u] = ((p[u] > a[u]) == keep_max) ? p[u] : a[u];
+        }
+#pragma unroll
+        for (int u = 0; u < QW; ++u) store(u, a[u]);
       } else {
 #pragma unroll 1
         for (int u = 0; u < QW; ++u) {
@@ -941,7 +973,8 @@ __global__ __launch_bounds__(kFusedWaves * 64) void catalog_fused(
                 __hip_atomic_load(src(u, sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             merge_keys_sel<32>(a, sl < S ? t : 0ull);
           }
-          finish(u, a);
+          merge_keys<32>(a, xor_lane64(a, 32));   // the odd lists' half into the even's
+          store(u, a);
         }
       }
       // re-arm the counter for the next call (stream order publishes it)

@@ -3,5 +3,5 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r06
-AB_DIR=abv bash scripts/diag/c3_libs6.sh ko1 ko2 > gpurun_out/r06/c3ko.txt 2>&1 || { tail -20 gpurun_out/r06/c3ko.txt; exit 1; }
+AB_DIR=abv bash scripts/diag/c3_libs6.sh ko4 ko2 > gpurun_out/r06/c3ko.txt 2>&1 || { tail -20 gpurun_out/r06/c3ko.txt; exit 1; }
 cat gpurun_out/r06/c3ko.txt
