@@ -105,8 +105,9 @@ size_t dfm_fused_pack_bytes(int L, const int32_t* dims, bool mlp_bf16);
 // base[m] = (Σ_f w·Wp + FM part) + bp into a.fm_out from the pair table
 // C = (E ⊙ Wp)·Eᵀ (dfm_fused.hip; built once per call into a.scratch); false
 // (nothing launched) when it does not fit a.scratch, the rows are too few to
-// pay for it, or the plan asks for HHFM_PLAN_ROW_FM
-bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st);
+// pay for it, or the plan asks for HHFM_PLAN_ROW_FM.  base = false: the table
+// only (the wide kernel forms the rows' base itself)
+bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st, bool base = true);
 // split-bf16 hidden layers for the fp32 MLP (no HHFM_PLAN_EXACT_FP32)
 inline bool dfm_f32_split(int32_t plan) { return !(plan & HHFM_PLAN_EXACT_FP32); }
 

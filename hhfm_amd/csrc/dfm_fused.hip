@@ -1451,7 +1451,7 @@ __global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restri
   base[m] = (y1 + y2) + bp;
 }
 
-bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
+bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st, bool base) {
   const int64_t M = a.M, B = a.B;
   const int k = a.k;
   const size_t cbytes = (size_t)M * M * 4, sbytes = (size_t)M * k * 4;
@@ -1479,8 +1479,9 @@ bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st) {
   launch_gemm(g, false, 0, st);
   if (a.pairs_ready) *a.pairs_ready = true;
   }
-  hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
-                     a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out);
+  if (base)
+    hipLaunchKernelGGL(dfm_fm_base_pairs, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, st,
+                       a.idx, B, a.F, M, a.w, a.Wp, a.bp, Cp, a.fm_out);
   return true;
 }
 
@@ -1830,7 +1831,11 @@ __global__ __launch_bounds__(256) void dfm_gather_rows(const int32_t* __restrict
 // identical either way.  Larger key ranges take hipCUB's radix sort.
 constexpr int kGroupBins = 8192;
 constexpr int kGroupRows = 8192;      // rows per histogram block
-constexpr int kScatterRows = 4096;    // rows per scatter block (<= 65536: 16-bit local index)
+// (8 K / 16 K rows per block: C5 bf16 within 0.03 ms, profiles/r06_wfb_ab.txt)
+#ifndef HHFM_SCATTER_ROWS
+#define HHFM_SCATTER_ROWS 4096
+#endif
+constexpr int kScatterRows = HHFM_SCATTER_ROWS;   // rows per scatter block (<= 65536: 16-bit local index)
 
 __global__ __launch_bounds__(1024) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
                                                       int F, int key_field, int64_t M,

@@ -83,6 +83,14 @@ namespace hhfm {
 #ifndef HHFM_WPI
 #define HHFM_WPI 1
 #endif
+// PAIRS: 0 = each row's base (Σ_f w·Wp + Σ_{f<g} C[x_f][x_g]) + bp read from
+// the dfm_fm_base_pairs launch's output; 1 = formed in the prologue from the
+// pair table in that kernel's order (bit-identical, but C5 bf16 9.96-9.98 ms
+// against 9.94-9.96: the kernel grew by the 0.28 ms the launch took — the
+// gathers are the same random C rows either way; profiles/r06_wfb_ab.txt)
+#ifndef HHFM_WFB
+#define HHFM_WFB 0
+#endif
 
 template <int B_, int E_, class Fn>
 HHFM_DEV void static_for(Fn&& fn) {
@@ -209,7 +217,7 @@ HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, 
   constexpr int kVl = kBl + 3 * NR * 4;
   constexpr int kWp = kVl + NR * 4;
   constexpr int kPlo = kWp + (kFusedMaxF + kFusedMaxK) * 4;
-  constexpr int kYl = kPlo + 5 * kFusedMaxF * 4;
+  constexpr int kYl = kPlo + 6 * kFusedMaxF * 4;
   constexpr int kPst = kYl + kWideRows * 4;
   constexpr int kPsLd = NR + 4;                        // staged P row stride (floats)
   constexpr int kPsFloats = (kLdsBytes - kPst) / 4;
@@ -219,7 +227,7 @@ HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, 
   float* blv = reinterpret_cast<float*>(smem + kBl);
   float* vl = reinterpret_cast<float*>(smem + kVl);
   float* wpl = reinterpret_cast<float*>(smem + kWp);
-  int32_t* plo = reinterpret_cast<int32_t*>(smem + kPlo);   // lo | hi | P | E | g base
+  int32_t* plo = reinterpret_cast<int32_t*>(smem + kPlo);   // lo | hi | P | E | g base | perm⁻¹
   float* ylds = reinterpret_cast<float*>(smem + kYl);
   float* pst = reinterpret_cast<float*>(smem + kPst);
 
@@ -246,6 +254,7 @@ HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, 
   if (tid < kFusedMaxF) {
     plo[tid] = 0x7fffffff;
     plo[kFusedMaxF + tid] = -1;
+    if (tid < F) plo[5 * kFusedMaxF + (int)((a.perm >> (4 * tid)) & 15)] = tid;
   }
   __syncthreads();
 
@@ -278,6 +287,21 @@ HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, 
     for (int f = 0; f < kFusedMaxF; ++f)
       if (f < F) y1 += wv8[f] * wpl[f];
     ylds[tid] = y1;
+  }
+  if (PAIRS && HHFM_WFB && tid < kWideRows) {   // the caller's field order, as dfm_fm_base_pairs
+    const float* C = reinterpret_cast<const float*>(a.scratch);
+    int32_t x[F];
+#pragma unroll
+    for (int c = 0; c < F; ++c) x[c] = ids[tid * F + plo[5 * kFusedMaxF + c]];
+    float y2 = 0.f;
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+      for (int g = f + 1; g < F; ++g) y2 += C[(int64_t)x[f] * a.M + x[g]];
+    float y1 = 0.f;
+#pragma unroll
+    for (int f = 0; f < F; ++f) y1 = __fmaf_rn(a.w[x[f]], a.Wp[f], y1);
+    ylds[tid] = (y1 + y2) + a.bp;
   }
   for (int x = tid; x < (OVF ? 0 : kWideRows * NF); x += NTH) {
     const int row = x / NF, f = 1 + x % NF;
@@ -655,7 +679,7 @@ HHFM_DEV void wide_rows(const FusedDfmArgs& a, const int64_t m0, uint32_t* ovf, 
       const int64_t m = m0 + row;
       if constexpr (ST && HHFM_WFM && !PAIRS) yy -= 0.5f * gh[rt];   // − ½ Σ_f g[x_f], staged fields
       if (le < 16 && m < a.B) {
-        if constexpr (PAIRS) a.out[a.order ? a.order[m] : m] = a.fmbase[m] + pt;
+        if constexpr (PAIRS) a.out[a.order ? a.order[m] : m] = (HHFM_WFB ? ylds[row] : a.fmbase[m]) + pt;
         else a.out[a.order ? a.order[m] : m] = ((ylds[row] + yy) + a.bp) + pt;
       }
     }
@@ -711,7 +735,7 @@ static void wide_launch_shape(const FusedDfmArgs& a, hipStream_t st) {
   const int64_t cap = ((int64_t)dfm_fused_pack_bytes(a.L, a.dims, true) - (int64_t)wbytes) / 4 -
                       kOvfHead;
   const int64_t chunk = cap / (kRowsWG / 64) * kRowsWG;   // units of >= 64 rows
-  const bool pairs = dfm_fm_pairs(a, true, st);
+  const bool pairs = dfm_fm_pairs(a, true, st, !HHFM_WFB);
   for (int64_t r0 = 0; r0 < a.B; r0 += chunk) {
     FusedDfmArgs c = a;
     c.B = a.B - r0 < chunk ? a.B - r0 : chunk;

@@ -13,7 +13,7 @@ from hhfm_amd.DFM import DeepFM
 
 out = {}
 for k, layers, B, grouped in [(64, [150] * 3, 777, False), (64, [150] * 3, 20000, True),
-                              (256, [400] * 3, 3000, False)]:
+                              (256, [400] * 3, 3000, False), (256, [400] * 3, 82000, True)]:
     rng = np.random.default_rng(k + B)
     nu, ni, ctx = 957, 4082, (7, 2, 3)
     M = nu + ni + sum(ctx)

@@ -48,19 +48,24 @@ def _slot(o, v):
 
 def _check_var(got, ref, before, o, grad):
     """_close_update, except under Adam: its early steps move an element by
-    ≈ ±α whatever |g| is, so an element whose gradient sits near the float
-    atomics' summation-order noise (|g| < 1e-4 of its table row's largest
-    |g|, of the whole variable's for a vector) may take the other sign; those
-    are held only to that bound (≤ 2 × the largest step)."""
+    ≈ ±α whatever |g| is, so its update error is ≈ 3·α_t·δg/|g| for a
+    gradient error δg (d(m̂/√v̂)/dg ≈ (1−β1)/√v̂, √v̂ ≥ √(1−β2)·|g|).  The
+    float atomics' summation order gives δg up to ~1e-6 of the table row's
+    largest |g| (the whole variable's for a vector), so elements with |g| ≥
+    1e-2 of that are held to 1e-4 of the largest step (a 1e-4 cut-off failed
+    once among round 6's GPU runs); the rest (~2 %) only to ≤ 2 × the largest step."""
     got, ref, before = (np.asarray(x, np.float32) for x in (got, ref, before))
     if o != "adam":
         _close_update(got, ref, before)
         return
     g = np.abs(np.asarray(grad, np.float32).reshape(ref.shape))
     scale = g.max(axis=-1, keepdims=True) if g.ndim == 2 else g.max(initial=0.0)
-    well = g >= 1e-4 * scale
+    well = g >= 1e-2 * scale
     step = np.abs(ref - before).max()
-    assert np.allclose(got[well], ref[well], rtol=1e-5, atol=1e-4 * step + 1e-9)
+    off = well & ~np.isclose(got, ref, rtol=1e-5, atol=1e-4 * step + 1e-9)
+    gs = g / np.maximum(scale, 1e-30)
+    assert not off.any(), (f"{off.sum()} elements: |g|/row max {gs[off][:8]}, "
+                           f"|got-ref| {np.abs(got - ref)[off][:8]}, step {step}")
     assert np.all(np.abs(got - ref) <= 2.01 * step + 1e-9)
     assert (well & (g > 0)).sum() >= 0.9 * (g > 0).sum()
 
