@@ -33,6 +33,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+if os.environ.get("HHFM_AB_ROOT"):   # diagnostic A/B: another build's package copy first
+    sys.path.insert(0, os.environ["HHFM_AB_ROOT"])
 
 METRIC = "scored (user,ctx,item) triples/sec + HR@10, Frappe-shape, 1/2/4/8 MI355X"
 BYTES_PER_ROW_F5_K64 = 5 * 64 * 4 + 5 * 4 + 5 * 4 + 4   # 1,324 B

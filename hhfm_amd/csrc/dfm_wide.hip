@@ -83,13 +83,14 @@ namespace hhfm {
 #ifndef HHFM_WPI
 #define HHFM_WPI 1
 #endif
-// PAIRS: 0 = each row's base (Σ_f w·Wp + Σ_{f<g} C[x_f][x_g]) + bp read from
-// the dfm_fm_base_pairs launch's output; 1 = formed in the prologue from the
-// pair table in that kernel's order (bit-identical, but C5 bf16 9.96-9.98 ms
-// against 9.94-9.96: the kernel grew by the 0.28 ms the launch took — the
-// gathers are the same random C rows either way; profiles/r06_wfb_ab.txt)
+// PAIRS: 1 = each row's base (Σ_f w·Wp + Σ_{f<g} C[x_f][x_g]) + bp formed in
+// the prologue from the pair table, in dfm_fm_base_pairs' order (the same
+// bits, tested); 0 = that launch's output read in the epilogue.  C5 bf16
+// 9.85 -> 9.74-9.76 ms per pass (profiles/r06_wfb_ab.txt): the 0.28-ms launch
+// and its round trip of the bases through HBM gone, its gathers now under
+// the other workgroup's MFMAs
 #ifndef HHFM_WFB
-#define HHFM_WFB 0
+#define HHFM_WFB 1
 #endif
 
 template <int B_, int E_, class Fn>

@@ -1,8 +1,9 @@
 #!/bin/bash
-# round 6: library builds abv/<name> given as arguments (e.g. wfb0: the
-# PAIRS base from the dfm_fm_base_pairs launch; sc8k / sc16k: 8 K / 16 K-row
+# round 6: library builds abv/<name> given as arguments (e.g. wfb1: the
+# PAIRS base formed in the wide kernel's prologue; sc8k / sc16k: 8 K / 16 K-row
 # grouping scatter blocks) against the tree: wide_probe.py outputs bit for
 # bit (incl. a PAIRS case), then the C5 bf16 leg of each build, twice
+# (bench.py puts the repo first on sys.path: the build goes in by HHFM_AB_ROOT)
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 o=gpurun_out/r06/wfb
@@ -14,7 +15,7 @@ for n in base "$@"; do
 done
 for n in "$@"; do python scripts/diag/wide_compare.py $o/base.npz $o/$n.npz; done
 for rep in 1 2; do for n in base "$@"; do
-  PYTHONPATH=/tmp/wv_$n timeout -k 10 300 python bench.py --legs c5 --no-pmc > $o/c5_$n.json 2> $o/c5_$n.err || { tail -20 $o/c5_$n.err; exit 1; }
+  HHFM_AB_ROOT=/tmp/wv_$n timeout -k 10 300 python bench.py --legs c5 --no-pmc > $o/c5_$n.json 2> $o/c5_$n.err || { tail -20 $o/c5_$n.err; exit 1; }
   python3 -c "
 import json
 d = json.loads(open('$o/c5_$n.json').read().strip().splitlines()[-1]); ex = d.get('extra', d)

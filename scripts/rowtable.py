@@ -20,6 +20,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+if os.environ.get("HHFM_AB_ROOT"):   # diagnostic A/B: another build's package copy first
+    sys.path.insert(0, os.environ["HHFM_AB_ROOT"])
 import bench  # noqa: E402
 from hhfm_amd import ops  # noqa: E402
 from oracle import cpu as ocpu  # noqa: E402
