@@ -60,6 +60,10 @@ struct FusedDfmArgs {
   // catalog's query chunks build it once)
   int32_t plan;
   bool* pairs_ready;
+  // per caller field f of this call's rows (dfm_order_rows): [2f] =
+  // 0x7fffffff − min id, [2f+1] = max id, or null; the pair table is then
+  // built only in the 128x128 tiles some field pair f < g reads
+  const int32_t* franges;
 };
 
 HHFM_DEV uint32_t pack_bf16x2(float lo, float hi) {   // v_cvt_pk_bf16_f32 (RNE)

@@ -1451,6 +1451,11 @@ __global__ __launch_bounds__(256) void dfm_fm_base_pairs(const int32_t* __restri
   base[m] = (y1 + y2) + bp;
 }
 
+// the pair table built only in the tiles the call's field ranges read
+// (HHFM_PAIRS_ALL_TILES=1: every tile — the same bits, A/B)
+#ifndef HHFM_PAIRS_ALL_TILES
+#define HHFM_PAIRS_ALL_TILES 0
+#endif
 bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st, bool base) {
   const int64_t M = a.M, B = a.B;
   const int k = a.k;
@@ -1476,6 +1481,10 @@ bool dfm_fm_pairs(const FusedDfmArgs& a, bool tbf, hipStream_t st, bool base) {
   g.b_src_bf16 = tbf;
   g.C = Cp;
   g.ldc = M;
+  if (a.franges && !a.pairs_ready && !(HHFM_PAIRS_ALL_TILES)) {   // this call's rows only
+    g.tile_ranges = a.franges;
+    g.tr_F = a.F;
+  }
   launch_gemm(g, false, 0, st);
   if (a.pairs_ready) *a.pairs_ready = true;
   }
@@ -1608,7 +1617,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
                       uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
-                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st) {
+                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st,
+                      const int32_t* franges) {
   if (!dfm_fused_eligible(L, dims) || F > kFusedMaxF || k > kFusedMaxK) return false;
   if (k % 16) return false;
   for (int i = 0; i < L; ++i)
@@ -1638,6 +1648,7 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
   a.fm_out = fm_base;
   a.plan = plan;
   a.pairs_ready = pairs_ready;
+  a.franges = franges;
   if (pj && (proj_from < 0 || proj_from >= F)) return false;
   if (!mlp_bf16) {
     // the fp32 kernel projects all fields, in the caller's order
@@ -1836,20 +1847,55 @@ constexpr int kGroupRows = 8192;      // rows per histogram block
 #endif
 constexpr int kScatterRows = HHFM_SCATTER_ROWS;   // rows per scatter block (<= 65536: 16-bit local index)
 
+// franges (or null, F <= kFusedMaxF): every field's id range over the rows
+// (FusedDfmArgs::franges encoding, global atomicMax onto zeros) — the same
+// lines the key column's reads fetch
 __global__ __launch_bounds__(1024) void dfm_group_hist(const int32_t* __restrict__ idx, int64_t B,
                                                       int F, int key_field, int64_t M,
-                                                      uint32_t* __restrict__ count) {
+                                                      uint32_t* __restrict__ count,
+                                                      int32_t* __restrict__ franges) {
   __shared__ uint32_t hcnt[kGroupBins];
+  __shared__ int32_t fr[2 * kFusedMaxF];
   const int nb = (int)M;
   for (int b = threadIdx.x; b < nb; b += 1024) hcnt[b] = 0;
+  if (threadIdx.x < 2 * kFusedMaxF) fr[threadIdx.x] = 0;
   __syncthreads();
   const int64_t r0 = (int64_t)blockIdx.x * kGroupRows;
   const int64_t r1 = r0 + kGroupRows < B ? r0 + kGroupRows : B;
-  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024)
+  int32_t rl[kFusedMaxF], rh[kFusedMaxF];
+#pragma unroll
+  for (int f = 0; f < kFusedMaxF; ++f) rl[f] = rh[f] = 0;
+  for (int64_t m = r0 + threadIdx.x; m < r1; m += 1024) {
     atomicAdd(&hcnt[clamp_id(idx[m * F + key_field], M)], 1u);
+    if (franges) {
+#pragma unroll
+      for (int f = 0; f < kFusedMaxF; ++f)
+        if (f < F) {
+          const int32_t v = clamp_id(idx[m * F + f], M);
+          rl[f] = max(rl[f], 0x7fffffff - v);
+          rh[f] = max(rh[f], v);
+        }
+    }
+  }
+  if (franges) {
+#pragma unroll
+    for (int f = 0; f < kFusedMaxF; ++f) {
+      if (f < F) {
+        for (int o = 32; o; o >>= 1) {
+          rl[f] = max(rl[f], __shfl_xor(rl[f], o, 64));
+          rh[f] = max(rh[f], __shfl_xor(rh[f], o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+          atomicMax(&fr[2 * f], rl[f]);
+          atomicMax(&fr[2 * f + 1], rh[f]);
+        }
+      }
+    }
+  }
   __syncthreads();
   for (int b = threadIdx.x; b < nb; b += 1024)
     if (hcnt[b]) atomicAdd(&count[b], hcnt[b]);
+  if (franges && threadIdx.x < 2 * F) atomicMax(&franges[threadIdx.x], fr[threadIdx.x]);
 }
 
 // exclusive scan of count[0, M) into start (one block)
@@ -1965,14 +2011,18 @@ size_t dfm_order_bytes(int64_t B, int F, int64_t M) {
                                              (uint32_t*)nullptr, (const int32_t*)nullptr,
                                              (int32_t*)nullptr, (int)B, 0, dfm_key_bits(M));
   else
-    tmp = 3 * dfm_al256((size_t)M * 4);
+    tmp = 3 * dfm_al256((size_t)M * 4) + dfm_al256(2 * kFusedMaxF * 4);
   return 4 * dfm_al256((size_t)B * 4) + dfm_al256((size_t)B * F * 4) + dfm_al256(tmp);
 }
 
 // Groups the rows by field key_field: returns the order (in ws) and the
 // regrouped rows in *rows_out, or null when B does not fit the sort's int.
+// franges_out (or null): the fields' id ranges when the counting sort ran
+// (FusedDfmArgs::franges), else null.
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
-                              void* ws, const int32_t** rows_out, hipStream_t st) {
+                              void* ws, const int32_t** rows_out, hipStream_t st,
+                              const int32_t** franges_out) {
+  if (franges_out) *franges_out = nullptr;
   if (B < 1 || B > 0x7fffffff) return nullptr;
   char* p = reinterpret_cast<char*>(ws);
   const size_t col = dfm_al256((size_t)B * 4);
@@ -1984,10 +2034,14 @@ const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_fiel
     uint32_t* count = reinterpret_cast<uint32_t*>(tmp_ws);
     uint32_t* cursor = reinterpret_cast<uint32_t*>(tmp_ws + mb);
     uint32_t* start = reinterpret_cast<uint32_t*>(tmp_ws + 2 * mb);
+    int32_t* fr = franges_out && F <= kFusedMaxF
+                      ? reinterpret_cast<int32_t*>(tmp_ws + 3 * mb) : nullptr;
     if (hipMemsetAsync(count, 0, 2 * mb, st) != hipSuccess) return nullptr;
+    if (fr && hipMemsetAsync(fr, 0, 2 * kFusedMaxF * 4, st) != hipSuccess) return nullptr;
     const unsigned nblk = (unsigned)((B + kGroupRows - 1) / kGroupRows);
     hipLaunchKernelGGL(dfm_group_hist, dim3(nblk), dim3(1024), 0, st, idx, B, F, key_field, M,
-                       count);
+                       count, fr);
+    if (fr) *franges_out = fr;
     hipLaunchKernelGGL(dfm_group_scan, dim3(1), dim3(1024), 0, st, count, M, start);
     const unsigned sblk = (unsigned)((B + kScatterRows - 1) / kScatterRows);
     hipLaunchKernelGGL(dfm_group_scatter, dim3(sblk), dim3(1024), 0, st, idx, B, F, key_field,

@@ -99,6 +99,11 @@ struct GemmArgs {
   int ksplit;           // split-K (epilogue 0): blockIdx.z covers K range
                         // [z*ksplit, (z+1)*ksplit), ksplit % 32 == 0, and
   int64_t cz_stride;    // stores to C + z*cz_stride (elements); 0 = no split
+  // FM pair table C[a][b] (dfm_fm_pairs): per field f, [2f] = 0x7fffffff − min
+  // id, [2f+1] = max id; a tile no (f < g) pair of ranges touches is skipped
+  // (its entries are never read).  Null: every tile.
+  const int32_t* tile_ranges;
+  int tr_F;
 };
 
 // (i, j) of pair p among i<j<F in the reference's loop order (AFM.py:107-110)
@@ -204,6 +209,18 @@ __global__ __launch_bounds__(256) void gemm_mfma(GemmArgs g) {
   const int wm = wv >> 1, wn = wv & 1;
   const int64_t m0 = (int64_t)blockIdx.x * GBM;
   const int n0 = blockIdx.y * GBN;
+  if (g.tile_ranges) {   // uniform: the whole block leaves before any barrier
+    bool need = false;
+    for (int f = 0; f + 1 < g.tr_F && !need; ++f) {
+      const int64_t flo = 0x7fffffff - g.tile_ranges[2 * f], fhi = g.tile_ranges[2 * f + 1];
+      if (fhi < m0 || flo >= m0 + GBM) continue;
+      for (int h = f + 1; h < g.tr_F && !need; ++h) {
+        const int hlo = 0x7fffffff - g.tile_ranges[2 * h], hhi = g.tile_ranges[2 * h + 1];
+        need = !(hhi < n0 || hlo >= n0 + GBN);
+      }
+    }
+    if (!need) return;
+  }
   const int kb = g.ksplit ? (int)blockIdx.z * g.ksplit : 0;
   const int ke = g.ksplit ? min(g.K, kb + g.ksplit) : g.K;
   const int nk = (ke - kb + BK - 1) / BK;

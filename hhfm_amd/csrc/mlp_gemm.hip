@@ -31,7 +31,8 @@ bool dfm_fused_launch(const int32_t* idx, int64_t B, int F, const void* E, int64
                       const void* const* Wt, const float* const* bias, const float* Wp, float bp,
                       float* out, void* pack_ws, const void* proj, int proj_from,
                       uint64_t perm, const int32_t* order, float* fm_base, void* scratch,
-                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st);
+                      size_t scratch_bytes, int32_t plan, bool* pairs_ready, hipStream_t st,
+                      const int32_t* franges);
 bool dfm_proj_eligible(int F, int k, int L, const int32_t* dims);
 size_t dfm_proj_bytes(int F, int proj_from, int64_t M, int L, const int32_t* dims);
 void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16, int F,
@@ -40,7 +41,8 @@ void dfm_project_layer0(const void* E, int64_t M, int k, bool tbf, bool mlp_bf16
 size_t dfm_order_bytes(int64_t B, int F, int64_t M);
 inline bool dfm_f32_split(int32_t plan) { return !(plan & HHFM_PLAN_EXACT_FP32); }
 const int32_t* dfm_order_rows(const int32_t* idx, int64_t B, int F, int key_field, int64_t M,
-                              void* ws, const int32_t** rows_out, hipStream_t st);
+                              void* ws, const int32_t** rows_out, hipStream_t st,
+                              const int32_t** franges_out);
 constexpr uint64_t kDfmIdentityPerm = 0xFEDCBA9876543210ull;
 
 // ---------------------------------------------------------------------------
@@ -236,7 +238,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
                             const float* const* bias, int32_t mlp_dtype, const float* Wp,
                             float bp, float* out, char* ws, const DfmPlan& p, const void* proj,
                             const int32_t* order, int32_t plan, bool* pairs_ready,
-                            hipStream_t st) {
+                            hipStream_t st, const int32_t* franges = nullptr) {
   const bool bf = mlp_dtype == HHFM_BF16;
   // One fused kernel per row block when the shape fits (dfm_fused.hip /
   // dfm_wide.hip, bf16 or fp32 MLP); the layer-by-layer GEMMs otherwise.
@@ -244,7 +246,7 @@ static int dfm_forward_impl(const int32_t* idx, int64_t B, int32_t F, const void
       dfm_fused_launch(idx, B, F, E, M, k, dtype == HHFM_BF16, bf, w, nlayers, dims, Wt, bias,
                        Wp, bp, out, ws + p.off_pack, proj, p.proj_from, p.perm, order,
                        reinterpret_cast<float*>(ws + p.off_base), ws + p.off_h0,
-                       p.off_pack - p.off_h0, plan, pairs_ready, st))
+                       p.off_pack - p.off_h0, plan, pairs_ready, st, franges))
     return (int)hipGetLastError();
   if (proj) return HHFM_EUNSUPPORTED;   // planned only inside the fused envelope
   float* base = reinterpret_cast<float*>(ws + p.off_base);
@@ -321,6 +323,7 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
                                char* ws, const DfmPlan& p, int32_t plan, hipStream_t st) {
   const void* proj = nullptr;
   const int32_t* order = nullptr;
+  const int32_t* franges = nullptr;
   if (p.proj) {
     dfm_project_layer0(E, features_M, k, dtype == HHFM_BF16, mlp_dtype == HHFM_BF16, F,
                        p.proj_from, p.perm, Wt[0], layer_dims[0], nlayers, layer_dims,
@@ -329,11 +332,12 @@ static int dfm_forward_planned(const int32_t* idx, int64_t B, int32_t F, const v
     const int32_t* grouped = nullptr;
     if (p.group)
       order = dfm_order_rows(idx, B, F, (int)((p.perm >> (4 * p.proj_from)) & 15), features_M,
-                             ws + p.off_order, &grouped, st);
+                             ws + p.off_order, &grouped, st, &franges);
     if (order) idx = grouped;
   }
   return dfm_forward_impl(idx, B, F, E, features_M, k, dtype, w, nlayers, layer_dims, Wt, bias,
-                          mlp_dtype, Wp, bp, out, ws, p, proj, order, plan, nullptr, st);
+                          mlp_dtype, Wp, bp, out, ws, p, proj, order, plan, nullptr, st,
+                          franges);
 }
 
 static int dfm_forward_args(const int32_t* idx, int64_t B, int32_t F, const void* E,
